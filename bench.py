@@ -1,0 +1,185 @@
+"""bench.py -- windows/s of the MI355X wake-word hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One step = one pass of the hot path (1 s @ 16 kHz audio -> MFCC (torchaudio
+definition + CMVN) -> xiaoa CNN -> logit, fp32) over one batch of B synthetic
+clips that are already resident in HBM (B = 65,536 per
+GPU).  Multi-GPU = one process per GPU, each rank takes its own contiguous
+range of global clip indices (weak scaling, no collective on the data path;
+torch.distributed is used only for the barrier and the max-over-ranks time).
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "esp32-wake-word_amd"))
+sys.path.insert(0, REPO)
+
+# Algorithmic work per window: front-end 960,744 + CNN 1,301,696 flop.
+FLOP_FE = 960_744
+FLOP_CNN = 1_301_696
+FLOP_PER_WINDOW = FLOP_FE + FLOP_CNN
+BYTES_PER_WINDOW_F32 = 64_004          # 16000 fp32 samples in + 1 fp32 logit out
+PEAK_FP32_TFLOPS = 157.3               # MI355X fp32 vector == fp32 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=65536, help="clips per GPU per step")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """The ml_models CPU path (torch fp32 restatement, oracle/wk_torch_cpu.py) on
+    the host cores, timed on a bounded sample of the same synthetic workload."""
+    import numpy as np
+    import torch
+    from oracle import wk_oracle as O
+    from oracle.wk_torch_cpu import TorchCpuPath
+    from wakeword.onnx_reader import read_onnx, xiaoa_state_dict
+    inits, _, _ = read_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"))
+    path = TorchCpuPath(xiaoa_state_dict(inits))
+    batch = 256
+    x = torch.from_numpy(O.synth_clips(1234, 0, batch))
+    path(x)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        path(x)
+        n += batch
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 4 * batch:
+            break
+    return {"value": round(n / el, 1), "unit": "windows/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{n} windows = {n // batch} batches of {batch} synthetic clips (seed 1234), "
+                      f"{el:.1f} s; torch-CPU fp32 restatement of the torchaudio MFCC+CMVN front-end "
+                      f"+ LightweightKWS on the xiaoa.onnx weights (oracle/wk_torch_cpu.py)"}
+
+
+def load_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    p = os.path.join(REPO, "profiles", "hbm_traffic.json")
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+        return d.get("bytes_per_window"), d.get("source")
+    except (OSError, ValueError):
+        return None, None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import wakeword
+    from wakeword import _lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"# note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    B = args.batch
+    model = wakeword.load_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"), device=local)
+    clips = wakeword.synth_clips(args.seed, rank * B, B, 16000, device=local)   # resident in HBM
+    logits = torch.empty((B,), dtype=torch.float32, device=f"cuda:{local}")
+    L = _lib.lib()
+    h = model._h.h
+    stream = torch.cuda.current_stream(local)
+    sptr = C.c_void_p(stream.cuda_stream)
+    aptr, lptr = C.c_void_p(clips.data_ptr()), C.c_void_p(logits.data_ptr())
+
+    def step():
+        st = L.wk_forward(h, aptr, _lib.WK_DTYPE_F32, B, 16000, 16000, lptr, None, sptr)
+        if st != 0:
+            _lib.check(st, "wk_forward")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, launch_ms = float(t[0]), float(t[1])
+    finite = bool(torch.isfinite(logits).all())
+
+    if rank == 0:
+        total = world * B * args.steps
+        value = total / elapsed
+        achieved = FLOP_PER_WINDOW * B / (launch_ms * 1e-3) / 1e12
+        traffic_bpw, traffic_src = load_traffic()
+        out = {
+            "metric": "audio windows/sec (1s@16kHz, 40-MFCC) through xiaoa CNN",
+            "value": round(value, 1),
+            "unit": "windows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: device counter-hash generator, clamp(0.1*N(0,1))+440 Hz sine on odd clips "
+                    "(SURVEY 8(d) config 2); xiaoa.onnx weights",
+            "config": {"workload": "config2: fused MFCC(torchaudio+CMVN)+xiaoa CNN fp32, B clips per GPU",
+                       "batch_per_gpu": B, "global_batch": world * B, "seq_len": 16000,
+                       "parallelism": f"dp{world} (per-rank clip split, no collectives)"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                         "traffic": (traffic_bpw * B if traffic_bpw else None),
+                         "launch_ms": round(launch_ms, 4),
+                         "flop_per_window": FLOP_PER_WINDOW,
+                         "hbm_gbs_algorithmic": round(BYTES_PER_WINDOW_F32 * B / (launch_ms * 1e-3) / 1e9, 1)},
+            "logits_finite": finite,
+        }
+        if traffic_src:
+            out["roofline"]["traffic_source"] = traffic_src
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,277 @@
+// wk_api.hip -- the C ABI of include/wakeword.h.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+#include <mutex>
+#include <string>
+
+#include "wakeword.h"
+#include "wk_kernels.h"
+
+struct wk_handle {
+  wk_config cfg;
+  int n_cu;
+  float* d_weights;      // packed WK_NUM_WEIGHTS floats, or nullptr (front-end only handle)
+  float* d_feats_ws;     // feature workspace for the unfused path
+  int64_t ws_clips;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+wk_status hip_fail(hipError_t e, const char* what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return WK_ERR_HIP;
+}
+
+wk_status invalid(const char* what) {
+  g_last_error = what;
+  return WK_ERR_INVALID_ARG;
+}
+
+// Run `body` with the handle's device current; restore the caller's device.
+template <typename F>
+wk_status on_device(int dev, F body) {
+  int old = -1;
+  hipError_t e = hipGetDevice(&old);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  if (old != dev && (e = hipSetDevice(dev)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+  wk_status s = body();
+  if (old != dev) (void)hipSetDevice(old);
+  return s;
+}
+
+constexpr int64_t kWorkspaceClips = 16384;
+
+}  // namespace
+
+extern "C" {
+
+int32_t wk_abi_version(void) { return WK_ABI_VERSION; }
+
+const char* wk_status_string(wk_status s) {
+  switch (s) {
+    case WK_OK: return "WK_OK";
+    case WK_ERR_INVALID_ARG: return "WK_ERR_INVALID_ARG";
+    case WK_ERR_HIP: return "WK_ERR_HIP";
+    case WK_ERR_NO_MEMORY: return "WK_ERR_NO_MEMORY";
+    case WK_ERR_UNSUPPORTED: return "WK_ERR_UNSUPPORTED";
+  }
+  return "WK_ERR_UNKNOWN";
+}
+
+const char* wk_last_error(void) { return g_last_error.c_str(); }
+
+wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle** out) {
+  if (!cfg || !out) return invalid("wk_create: null cfg/out");
+  *out = nullptr;
+  if (cfg->mode != WK_MODE_TORCHAUDIO_CMVN && cfg->mode != WK_MODE_ESP_MFCC) return invalid("wk_create: bad mode");
+  if (cfg->precision != WK_PREC_FP32 && cfg->precision != WK_PREC_BF16) return invalid("wk_create: bad precision");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  if (cfg->device < 0 || cfg->device >= ndev) return invalid("wk_create: device ordinal out of range");
+  wk_handle* h = (wk_handle*)calloc(1, sizeof(wk_handle));
+  if (!h) return WK_ERR_NO_MEMORY;
+  h->cfg = *cfg;
+  wk_status st = on_device(cfg->device, [&]() -> wk_status {
+    hipDeviceProp_t prop;
+    hipError_t e2 = hipGetDeviceProperties(&prop, cfg->device);
+    if (e2 != hipSuccess) return hip_fail(e2, "hipGetDeviceProperties");
+    h->n_cu = prop.multiProcessorCount;
+    if (host_weights) {
+      if ((e2 = hipMalloc(&h->d_weights, sizeof(float) * WK_NUM_WEIGHTS)) != hipSuccess)
+        return hip_fail(e2, "hipMalloc(weights)");
+      if ((e2 = hipMemcpy(h->d_weights, host_weights, sizeof(float) * WK_NUM_WEIGHTS, hipMemcpyHostToDevice)) !=
+          hipSuccess)
+        return hip_fail(e2, "hipMemcpy(weights)");
+      h->ws_clips = kWorkspaceClips;
+      if ((e2 = hipMalloc(&h->d_feats_ws, sizeof(float) * 13 * 63 * h->ws_clips)) != hipSuccess)
+        return hip_fail(e2, "hipMalloc(workspace)");
+    }
+    return WK_OK;
+  });
+  if (st != WK_OK) {
+    wk_destroy(h);
+    return st;
+  }
+  *out = h;
+  return WK_OK;
+}
+
+wk_status wk_destroy(wk_handle* h) {
+  if (!h) return WK_OK;
+  on_device(h->cfg.device, [&]() -> wk_status {
+    if (h->d_weights) (void)hipFree(h->d_weights);
+    if (h->d_feats_ws) (void)hipFree(h->d_feats_ws);
+    return WK_OK;
+  });
+  free(h);
+  return WK_OK;
+}
+
+static wk_status check_audio(const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len, int64_t clip_stride,
+                             bool mode_b) {
+  if (batch < 0) return invalid("batch < 0");
+  if (batch > 0 && !d_audio) return invalid("null audio pointer");
+  if (dtype != WK_DTYPE_F32 && dtype != WK_DTYPE_I16) return invalid("bad dtype");
+  if (mode_b && win_len != WK_WIN_SAMPLES) return invalid("mode B (torchaudio+CMVN) requires win_len == 16000");
+  if (!mode_b && win_len < 320) return invalid("mode A requires win_len >= 320");
+  if (clip_stride < win_len) return invalid("clip_stride < win_len");
+  return WK_OK;
+}
+
+wk_status wk_mfcc(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len,
+                  int64_t clip_stride, float* d_feats, void* stream) {
+  if (!h) return invalid("wk_mfcc: null handle");
+  const bool mode_b = h->cfg.mode == WK_MODE_TORCHAUDIO_CMVN;
+  wk_status s = check_audio(d_audio, dtype, batch, win_len, clip_stride, mode_b);
+  if (s != WK_OK) return s;
+  if (batch > 0 && !d_feats) return invalid("wk_mfcc: null feats");
+  return on_device(h->cfg.device, [&]() -> wk_status {
+    hipError_t e = wk::launch_frontend(mode_b, dtype == WK_DTYPE_I16, d_audio, batch, win_len, clip_stride, d_feats,
+                                       h->cfg.esp_dsp_packing, h->cfg.cmvn, 2 * h->n_cu, (hipStream_t)stream);
+    return e == hipSuccess ? WK_OK : hip_fail(e, "frontend launch");
+  });
+}
+
+wk_status wk_cnn(wk_handle* h, const float* d_feats, int64_t batch, float* d_logits, void* stream) {
+  if (!h) return invalid("wk_cnn: null handle");
+  if (!h->d_weights) return invalid("wk_cnn: handle created without weights");
+  if (batch < 0 || (batch > 0 && (!d_feats || !d_logits))) return invalid("wk_cnn: bad arguments");
+  if (h->cfg.precision == WK_PREC_BF16) {
+    g_last_error = "bf16 CNN not implemented in this build";
+    return WK_ERR_UNSUPPORTED;
+  }
+  return on_device(h->cfg.device, [&]() -> wk_status {
+    hipError_t e = wk::launch_cnn(d_feats, batch, h->d_weights, d_logits, false, h->n_cu, (hipStream_t)stream);
+    return e == hipSuccess ? WK_OK : hip_fail(e, "cnn launch");
+  });
+}
+
+wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len,
+                     int64_t clip_stride, float* d_logits, float* d_feats_or_null, void* stream) {
+  if (!h) return invalid("wk_forward: null handle");
+  if (h->cfg.mode != WK_MODE_TORCHAUDIO_CMVN) {
+    g_last_error = "wk_forward: the xiaoa CNN consumes mode-B (torchaudio+CMVN) features";
+    return WK_ERR_UNSUPPORTED;
+  }
+  if (!h->d_weights) return invalid("wk_forward: handle created without weights");
+  wk_status s = check_audio(d_audio, dtype, batch, win_len, clip_stride, true);
+  if (s != WK_OK) return s;
+  if (batch > 0 && !d_logits) return invalid("wk_forward: null logits");
+  if (h->cfg.precision == WK_PREC_BF16) {
+    g_last_error = "bf16 CNN not implemented in this build";
+    return WK_ERR_UNSUPPORTED;
+  }
+  return on_device(h->cfg.device, [&]() -> wk_status {
+    const size_t esz = dtype == WK_DTYPE_I16 ? 2 : 4;
+    for (int64_t c0 = 0; c0 < batch; c0 += h->ws_clips) {
+      const int64_t n = batch - c0 < h->ws_clips ? batch - c0 : h->ws_clips;
+      float* feats = d_feats_or_null ? d_feats_or_null + c0 * 13 * 63 : h->d_feats_ws;
+      const void* a = (const char*)d_audio + (size_t)(c0 * clip_stride) * esz;
+      hipError_t e = wk::launch_frontend(true, dtype == WK_DTYPE_I16, a, n, win_len, clip_stride, feats, 0, 1,
+                                         2 * h->n_cu, (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(e, "frontend launch");
+      e = wk::launch_cnn(feats, n, h->d_weights, d_logits + c0, false, h->n_cu, (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(e, "cnn launch");
+    }
+    return WK_OK;
+  });
+}
+
+wk_status wk_synth_clips(uint32_t seed, int64_t first, int64_t count, int32_t n, float* d_out, void* stream) {
+  if (count < 0 || n <= 0 || (count > 0 && !d_out)) return invalid("wk_synth_clips: bad arguments");
+  hipError_t e = wk::launch_synth(seed, first, count, n, d_out, (hipStream_t)stream);
+  return e == hipSuccess ? WK_OK : hip_fail(e, "synth launch");
+}
+
+wk_status wk_normalize(const float* d_in, float* d_out, int64_t batch, int32_t n_coef, int32_t n_time,
+                       int32_t method, void* stream) {
+  if (batch < 0 || n_coef <= 0 || n_time <= 1 || method < 0 || method > 3) return invalid("wk_normalize: bad args");
+  if (batch > 0 && (!d_in || !d_out)) return invalid("wk_normalize: null pointer");
+  hipError_t e = wk::launch_normalize(d_in, d_out, batch, n_coef, n_time, method, (hipStream_t)stream);
+  return e == hipSuccess ? WK_OK : hip_fail(e, "normalize launch");
+}
+
+// ---------------------------------------------------------------------------
+// mfcc.h compatibility shims (main/esp_mfcc/mfcc.h:10-17, mfcc.c:431-563).
+// ---------------------------------------------------------------------------
+static std::mutex g_compat_mu;
+static wk_handle* g_compat = nullptr;
+
+float* extract_mfcc(const float* signal, int signal_len, int sampling_rate, int frame_size, int hop_size, int n_fft,
+                    int n_filters, int n_mfcc) {
+  // mfcc.c:434-437: NULL signal or a signal shorter than one frame -> NULL.
+  if (!signal || signal_len < frame_size || frame_size <= 0) {
+    fprintf(stderr, "E (MFCC) Invalid signal parameters\n");
+    return nullptr;
+  }
+  if (sampling_rate != 16000 || frame_size != 320 || hop_size != 256 || n_fft != 512 || n_filters != 40 ||
+      n_mfcc != 13) {
+    fprintf(stderr, "E (MFCC) unsupported configuration (supported: 16000/320/256/512/40/13)\n");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(g_compat_mu);
+  if (!g_compat) {
+    wk_config cfg = {WK_MODE_ESP_MFCC, WK_PREC_FP32, 1, 0, 0};
+    if (wk_create(&cfg, nullptr, &g_compat) != WK_OK) {
+      fprintf(stderr, "E (MFCC) device init failed: %s\n", wk_last_error());
+      return nullptr;
+    }
+  }
+  const int nf = (signal_len - frame_size) / hop_size + 1;
+  float* host_out = (float*)malloc(sizeof(float) * (size_t)nf * n_mfcc);
+  if (!host_out) return nullptr;
+  float *d_sig = nullptr, *d_out = nullptr;
+  bool ok = false;
+  wk_status st = on_device(0, [&]() -> wk_status {
+    if (hipMalloc(&d_sig, sizeof(float) * signal_len) != hipSuccess) return WK_ERR_NO_MEMORY;
+    if (hipMalloc(&d_out, sizeof(float) * (size_t)nf * n_mfcc) != hipSuccess) return WK_ERR_NO_MEMORY;
+    if (hipMemcpy(d_sig, signal, sizeof(float) * signal_len, hipMemcpyHostToDevice) != hipSuccess) return WK_ERR_HIP;
+    wk_status s = wk_mfcc(g_compat, d_sig, WK_DTYPE_F32, 1, signal_len, signal_len, d_out, nullptr);
+    if (s != WK_OK) return s;
+    if (hipMemcpy(host_out, d_out, sizeof(float) * (size_t)nf * n_mfcc, hipMemcpyDeviceToHost) != hipSuccess)
+      return WK_ERR_HIP;
+    ok = true;
+    return WK_OK;
+  });
+  on_device(0, [&]() -> wk_status {
+    if (d_sig) (void)hipFree(d_sig);
+    if (d_out) (void)hipFree(d_out);
+    return WK_OK;
+  });
+  if (st != WK_OK || !ok) {
+    fprintf(stderr, "E (MFCC) extract_mfcc failed: %s\n", wk_last_error());
+    free(host_out);
+    return nullptr;
+  }
+  return host_out;
+}
+
+void free_mfcc(float* mfcc) { free(mfcc); }
+
+// mfcc.c:530-553: min/max/avg over the finite entries.
+void analyze_mfcc_range(float* mfcc, int size, const char* label) {
+  if (!mfcc || size <= 0) return;
+  float mn = INFINITY, mx = -INFINITY, sum = 0.0f;
+  int valid = 0;
+  for (int i = 0; i < size; i++) {
+    if (!isnan(mfcc[i]) && !isinf(mfcc[i])) {
+      if (mfcc[i] < mn) mn = mfcc[i];
+      if (mfcc[i] > mx) mx = mfcc[i];
+      sum += mfcc[i];
+      valid++;
+    }
+  }
+  if (valid > 0)
+    printf("I (MFCC) %s MFCC Range: min=%.6f, max=%.6f, avg=%.6f, valid=%d/%d\n", label ? label : "", mn, mx,
+           sum / valid, valid, size);
+  else
+    fprintf(stderr, "E (MFCC) %s MFCC: No valid values\n", label ? label : "");
+}
+
+}  // extern "C"

@@ -1,0 +1,104 @@
+// wk_misc.hip -- device-side synthetic clip generator and normalize_mfcc.
+#include "wk_common.h"
+#include "wk_kernels.h"
+
+using namespace wk;
+
+namespace {
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// clamp(0.1*N(0,1), -1, 1) (+ 0.1*sin(2*pi*440 t / 16000)
+// on odd clips); N(0,1) by Box-Muller on a counter hash of (seed, clip, sample).
+// Same arithmetic as oracle/wk_oracle.py:synth_clips.
+__global__ void wk_synth_kernel(uint32_t seed, int64_t first, int64_t count, int n, float* __restrict__ out) {
+  const int64_t total = count * (int64_t)n;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = idx / n;
+    const uint32_t s = (uint32_t)(idx - c * n);
+    const uint64_t clip = (uint64_t)(first + c);
+    const uint32_t key = mix32(seed ^ (uint32_t)(clip * 0x9E3779B9ull));
+    const uint32_t h1 = mix32(key ^ (s * 2u + 0x68E31DA4u));
+    const uint32_t h2 = mix32(h1 ^ 0xB5297A4Du);
+    const float u1 = ((float)(h1 >> 8) + 1.0f) * (1.0f / 16777216.0f);
+    const float u2 = (float)(h2 >> 8) * (1.0f / 16777216.0f);
+    const float r = sqrtf(-2.0f * logf(u1));
+    const float gs = r * cosf(6.2831853071795865f * u2);
+    float x = fminf(fmaxf(0.1f * gs, -1.0f), 1.0f);
+    if (clip & 1) {
+      const float ph = (float)((s * 440u) % 16000u) * (1.0f / 16000.0f);
+      x += 0.1f * sinf(6.2831853071795865f * ph);
+    }
+    out[idx] = x;
+  }
+}
+
+// normalize_mfcc (ml_models/src/extract_mfcc.py:47-88), one wave per row.
+__global__ void wk_normalize_kernel(const float* __restrict__ in, float* __restrict__ out, int64_t rows, int n,
+                                    int method) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* x = in + row * n;
+  float* y = out + row * n;
+  if (method == 0 || method == 2) {  // standardization / cmvn (identical in the reference)
+    float s = 0.0f;
+    for (int i = lane; i < n; i += 64) s += x[i];
+    const float mean = wave_sum(s) / (float)n;
+    float q = 0.0f;
+    for (int i = lane; i < n; i += 64) {
+      const float d = x[i] - mean;
+      q = __builtin_fmaf(d, d, q);
+    }
+    float sd = sqrtf(wave_sum(q) / (float)(n - 1));
+    sd = sd == 0.0f ? 1.0f : sd;
+    for (int i = lane; i < n; i += 64) y[i] = (x[i] - mean) / (sd + 1e-8f);
+  } else if (method == 1) {  // minmax
+    float mn = INFINITY, mx = -INFINITY;
+    for (int i = lane; i < n; i += 64) {
+      mn = fminf(mn, x[i]);
+      mx = fmaxf(mx, x[i]);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      mn = fminf(mn, __shfl_xor(mn, m, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+    }
+    for (int i = lane; i < n; i += 64) y[i] = (x[i] - mn) / (mx - mn + 1e-8f);
+  } else {
+    for (int i = lane; i < n; i += 64) y[i] = x[i];
+  }
+}
+
+}  // namespace
+
+namespace wk {
+
+hipError_t launch_synth(uint32_t seed, int64_t first, int64_t count, int n, float* out, hipStream_t stream) {
+  const int64_t total = count * (int64_t)n;
+  if (total == 0) return hipSuccess;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(wk_synth_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, seed, first, count, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_normalize(const float* in, float* out, int64_t batch, int n_coef, int n_time, int method,
+                            hipStream_t stream) {
+  const int64_t rows = batch * n_coef;
+  if (rows == 0) return hipSuccess;
+  const int64_t blocks = (rows + 3) / 4;
+  hipLaunchKernelGGL(wk_normalize_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, in, out, rows, n_time,
+                     method);
+  return hipGetLastError();
+}
+
+}  // namespace wk

@@ -1,0 +1,68 @@
+"""Build libwakeword.so (all HIP kernels + the C ABI) for gfx950, in-tree.
+
+    python -m wakeword.build          (from esp32-wake-word_amd/)
+
+hipcc cross-compiles for gfx950 without a GPU.  Objects are compiled in
+parallel and linked into ``wakeword/libwakeword.so`` next to this file, so
+the library travels with the repository snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)                       # esp32-wake-word_amd/
+REPO = os.path.dirname(ROOT)
+CSRC = os.path.join(ROOT, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+LIB = os.path.join(PKG, "libwakeword.so")
+OBJDIR = os.path.join(ROOT, "build")
+SOURCES = ["wk_frontend.hip", "wk_cnn.hip", "wk_misc.hip", "wk_api.hip"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("WK_OFFLOAD_ARCH", "gfx950")
+CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-fno-signed-zeros", "-ffp-contract=fast",
+          "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", CSRC]
+
+
+def _compile(src: str, extra) -> str:
+    obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+    cmd = [HIPCC, *CFLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed on {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if r.stderr.strip():
+        sys.stderr.write(r.stderr)
+    return obj
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "wakeword.h"), __file__]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, extra=()) -> str:
+    if not force and not _stale():
+        return LIB
+    if shutil.which(HIPCC) is None and not os.path.exists(HIPCC):
+        raise RuntimeError(f"hipcc not found ({HIPCC})")
+    os.makedirs(OBJDIR, exist_ok=True)
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, list(extra)), SOURCES))
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

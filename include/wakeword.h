@@ -1,0 +1,127 @@
+/*
+ * wakeword.h -- C ABI of the MI355X (gfx950) wake-word inference path.
+ *
+ * Drop-in boundary for the reference's hot path (Socrates666/esp32-wake-word):
+ *   audio window -> MFCC front-end -> xiaoa CNN (LightweightKWS) -> logit.
+ * Everything here is plain C: pointers, sizes, status codes; no C++ or torch
+ * types cross the boundary.  Device pointers are HIP device memory; `stream`
+ * is a hipStream_t passed as void* (NULL = the legacy default stream).
+ * Calls that take device pointers are stream-ordered, allocate nothing and
+ * never block the host.  Errors are reported as wk_status codes, never aborts.
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   - main/esp_mfcc/mfcc.h:10-17   extract_mfcc / free_mfcc / analyze_mfcc_range
+ *                                  (identical signatures and ownership below)
+ *   - ml_models/src/wakeModel.py:29-34  LightweightKWS.forward (wk_cnn)
+ *   - ml_models/src/extract_mfcc.py:137-175  MFCC + CMVN front-end (wk_mfcc)
+ *   - main/hello_world_main.cpp:183-267 / esp_wake_word_detector.cpp:154-228
+ *     per-window MFCC -> model->run() -> sigmoid (wk_forward)
+ */
+#ifndef WAKEWORD_H_
+#define WAKEWORD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WK_ABI_VERSION 1
+
+typedef enum {
+  WK_OK = 0,
+  WK_ERR_INVALID_ARG = 1,   /* null pointer, bad size, unsupported parameter combo */
+  WK_ERR_HIP = 2,           /* a HIP runtime call failed (see wk_last_error())     */
+  WK_ERR_NO_MEMORY = 3,     /* device or host allocation failed                    */
+  WK_ERR_UNSUPPORTED = 4    /* valid request this build does not implement         */
+} wk_status;
+
+/* Front-end definitions. */
+typedef enum {
+  WK_MODE_TORCHAUDIO_CMVN = 0, /* mode B: extract_mfcc.py:137-175 (+ CMVN), out [13][63] */
+  WK_MODE_ESP_MFCC = 1         /* mode A: esp_mfcc/mfcc.c:431-527, out [n_frames][13]     */
+} wk_mode;
+
+typedef enum { WK_DTYPE_F32 = 0, WK_DTYPE_I16 = 1 } wk_dtype;   /* audio sample type */
+typedef enum { WK_PREC_FP32 = 0, WK_PREC_BF16 = 1 } wk_precision; /* CNN arithmetic    */
+
+typedef struct {
+  int32_t mode;            /* wk_mode                                               */
+  int32_t precision;       /* wk_precision (front-end is always fp32)               */
+  int32_t esp_dsp_packing; /* mode A only: 1 = emulate dsps_cplx2reC_fc32 packing    */
+  int32_t device;          /* HIP device ordinal the handle binds to                */
+  int32_t cmvn;            /* mode B only: 1 = normalize_mfcc('cmvn') (the training */
+                           /* path, extract_mfcc.py:175), 0 = raw MFCC              */
+} wk_config;
+
+typedef struct wk_handle wk_handle;
+
+/* Number of floats in the packed weight blob wk_create() expects:
+ * conv_layers.0.weight [32][13][3], conv_layers.3.weight [64][32][3],
+ * conv_layers.6.weight [128][64][3], classifier.0.weight [64][128],
+ * classifier.2.weight [1][64] -- PyTorch state-dict layouts, concatenated. */
+#define WK_NUM_WEIGHTS 40224
+
+/* Fixed geometry of the xiaoa model (1 s @ 16 kHz). */
+#define WK_WIN_SAMPLES 16000
+#define WK_N_MFCC 13
+#define WK_N_FRAMES_B 63
+
+/* Create a handle on cfg->device.  `host_weights` (WK_NUM_WEIGHTS floats, host
+ * memory) may be NULL for a front-end-only handle.  Replaces the reference's
+ * `new dl::Model(...)` + weight load (hello_world_main.cpp:178). */
+wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle** out);
+wk_status wk_destroy(wk_handle* h);
+
+/* Front-end only.  d_audio: `batch` clips of `win_len` samples, clip i at
+ * d_audio + i*clip_stride elements (dtype WK_DTYPE_F32 or WK_DTYPE_I16; i16 is
+ * scaled by 1/32768 like torchaudio.load).  Mode B requires win_len == 16000
+ * and writes CMVN'd features [batch][13][63]; mode A accepts win_len >= 320
+ * and writes [batch][n_frames][13] with n_frames = (win_len-320)/256+1. */
+wk_status wk_mfcc(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len,
+                  int64_t clip_stride, float* d_feats, void* stream);
+
+/* CNN only: d_feats [batch][13][63] -> d_logits [batch] (LightweightKWS.forward). */
+wk_status wk_cnn(wk_handle* h, const float* d_feats, int64_t batch, float* d_logits, void* stream);
+
+/* Fused hot path: audio -> logits [batch]; mode B only (the model's training
+ * front-end).  d_feats_or_null, when given, receives the [batch][13][63]
+ * features as well. */
+wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len,
+                     int64_t clip_stride, float* d_logits, float* d_feats_or_null, void* stream);
+
+/* Device-side synthetic clip generator: fills
+ * d_out[count][n] with clips first..first+count-1 of the counter-based
+ * generator keyed on `seed` (bit-compatible with oracle.synth_clips up to
+ * libm rounding). */
+wk_status wk_synth_clips(uint32_t seed, int64_t first, int64_t count, int32_t n, float* d_out, void* stream);
+
+/* normalize_mfcc(mfcc, method) (extract_mfcc.py:47-88) on device:
+ * d_in/d_out [batch][n_coef][n_time]; method 0 = 'standardization',
+ * 1 = 'minmax', 2 = 'cmvn', 3 = passthrough. In-place allowed. */
+wk_status wk_normalize(const float* d_in, float* d_out, int64_t batch, int32_t n_coef, int32_t n_time,
+                       int32_t method, void* stream);
+
+/* Human-readable text for a status / the last HIP error seen by this thread. */
+const char* wk_status_string(wk_status s);
+const char* wk_last_error(void);
+int32_t wk_abi_version(void);
+
+/* ---- mfcc.h compatibility shims (main/esp_mfcc/mfcc.h:10-17) --------------
+ * Same signatures and ownership as the reference: host signal in, a malloc'd
+ * host block of n_frames*n_mfcc floats (frame-major) out, caller frees it with
+ * free_mfcc(); NULL on bad arguments.  Computed by the mode-A HIP kernel on
+ * device 0 (esp_dsp_packing on).  Only the reference's own configuration
+ * (16000 Hz, 320/256/512, 40 filters, 13 coefficients) is supported; other
+ * parameters return NULL. */
+float* extract_mfcc(const float* signal, int signal_len, int sampling_rate, int frame_size, int hop_size,
+                    int n_fft, int n_filters, int n_mfcc);
+void free_mfcc(float* mfcc);
+void analyze_mfcc_range(float* mfcc, int size, const char* label);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WAKEWORD_H_ */

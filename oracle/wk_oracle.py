@@ -1,0 +1,229 @@
+"""CPU ORACLE for the wake-word hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker / the timed CPU baseline.
+The product path (``esp32-wake-word_amd/wakeword`` + ``libwakeword.so``) never
+imports or calls anything in ``oracle/``.
+
+What it restates (float64 numpy, citations are to /root/reference):
+
+* Front-end mode B, the training front-end the xiaoa CNN was fit to:
+  ``ml_models/src/extract_mfcc.py:137-175`` -> torchaudio
+  ``functional.preemphasis`` (:171) + ``transforms.MFCC`` (:137-148) +
+  ``normalize_mfcc(method='cmvn')`` (:73-80).  torchaudio is a third-party
+  dependency that is absent from this image (unpinned version, torchaudio 2.x
+  semantics restated: Spectrogram(center=True, pad_mode='reflect', periodic
+  window zero-padded to n_fft centred), MelScale(htk, norm=None),
+  AmplitudeToDB is NOT used because log_mels=True -> ln(mel + 1e-6),
+  create_dct(norm='ortho')).
+  PARITY STATUS: no reference test or fixture holds torchaudio MFCC values, so
+  the front-end restatement is "parity unpinned" at the torchaudio boundary;
+  it is pinned indirectly (KAT statistics, detections on the reference WAVs)
+  and cross-checked against torch.stft in tests/golden/make_golden.py.
+
+* The xiaoa CNN ``LightweightKWS`` (``ml_models/src/wakeModel.py:4-34``) with
+  the ``ml_models/xiaoa.onnx`` weights.  PINNED: golden logits in
+  tests/golden were produced by importing the reference's own class.
+
+* The GRU-CTC head (``ml_models/ctc.py:82-152,453-471``) lives in
+  ``oracle/wk_ctc_oracle.py``; front-end mode A (``main/esp_mfcc/mfcc.c``) is
+  the C restatement ``oracle/esp_mfcc_oracle.c``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SAMPLE_RATE = 16000
+WIN_SAMPLES = 16000
+N_FFT = 512
+WIN_LENGTH = 320
+HOP = 256
+N_MELS = 40
+N_MFCC = 13
+N_FRAMES = 1 + WIN_SAMPLES // HOP  # 63 with center=True
+
+
+# --------------------------------------------------------------------------
+# B0: pad / trim (extract_mfcc.py:7-23)
+# --------------------------------------------------------------------------
+def pad_audio(audio: np.ndarray, target_length: int = WIN_SAMPLES, noise: np.ndarray | None = None) -> np.ndarray:
+    """extract_mfcc.py:7-23.  ``noise`` is the pre-drawn N(0,1)*0.005 pad (the
+    reference draws it with torch.randn); None -> zero pad (add_noise_to_pad=False)."""
+    audio = np.asarray(audio, dtype=np.float32)
+    n = audio.shape[-1]
+    if n > target_length:
+        return audio[..., :target_length].copy()
+    if n < target_length:
+        pad = np.zeros(target_length - n, np.float32) if noise is None else np.asarray(noise, np.float32)
+        return np.concatenate([audio, pad], axis=-1)
+    return audio.copy()
+
+
+# --------------------------------------------------------------------------
+# B1: preemphasis (torchaudio.functional.preemphasis, extract_mfcc.py:171)
+# --------------------------------------------------------------------------
+def preemphasis(x: np.ndarray, coeff: float = 0.97) -> np.ndarray:
+    x = np.asarray(x, np.float64)
+    y = x.copy()
+    y[..., 1:] -= coeff * x[..., :-1]
+    return y
+
+
+# --------------------------------------------------------------------------
+# B2: Spectrogram (power=2, center/reflect, periodic hamming(320) in 512)
+# --------------------------------------------------------------------------
+def hamming_periodic(n: int) -> np.ndarray:
+    k = np.arange(n, dtype=np.float64)
+    return 0.54 - 0.46 * np.cos(2.0 * np.pi * k / n)
+
+
+def power_spectrogram(y: np.ndarray) -> np.ndarray:
+    """(..., L) -> (..., T, 257) power |X|^2, torch.stft(center=True, reflect)."""
+    y = np.asarray(y, np.float64)
+    pad = N_FFT // 2
+    yp = np.pad(y, [(0, 0)] * (y.ndim - 1) + [(pad, pad)], mode="reflect")
+    n_frames = 1 + (yp.shape[-1] - N_FFT) // HOP
+    win = np.zeros(N_FFT)
+    left = (N_FFT - WIN_LENGTH) // 2
+    win[left:left + WIN_LENGTH] = hamming_periodic(WIN_LENGTH)
+    idx = np.arange(n_frames)[:, None] * HOP + np.arange(N_FFT)[None, :]
+    frames = yp[..., idx] * win
+    spec = np.fft.rfft(frames, n=N_FFT, axis=-1)
+    return spec.real ** 2 + spec.imag ** 2
+
+
+# --------------------------------------------------------------------------
+# B3: MelScale fbanks (htk, norm=None)
+# --------------------------------------------------------------------------
+def _hz_to_mel_htk(f):
+    return 2595.0 * np.log10(1.0 + np.asarray(f, np.float64) / 700.0)
+
+
+def _mel_to_hz_htk(m):
+    return 700.0 * (10.0 ** (np.asarray(m, np.float64) / 2595.0) - 1.0)
+
+
+def melscale_fbanks(n_freqs: int = N_FFT // 2 + 1, f_min: float = 0.0, f_max: float = SAMPLE_RATE / 2,
+                    n_mels: int = N_MELS, sample_rate: int = SAMPLE_RATE) -> np.ndarray:
+    """(n_freqs, n_mels) triangular HTK filterbank, no area normalisation."""
+    all_freqs = np.linspace(0, sample_rate // 2, n_freqs)
+    m_pts = np.linspace(_hz_to_mel_htk(f_min), _hz_to_mel_htk(f_max), n_mels + 2)
+    f_pts = _mel_to_hz_htk(m_pts)
+    f_diff = f_pts[1:] - f_pts[:-1]
+    slopes = f_pts[None, :] - all_freqs[:, None]
+    down = (-1.0 * slopes[:, :-2]) / f_diff[:-1]
+    up = slopes[:, 2:] / f_diff[1:]
+    return np.maximum(0.0, np.minimum(down, up))
+
+
+# --------------------------------------------------------------------------
+# B5: DCT-II ortho (create_dct)
+# --------------------------------------------------------------------------
+def create_dct(n_mfcc: int = N_MFCC, n_mels: int = N_MELS) -> np.ndarray:
+    """(n_mels, n_mfcc) DCT-II matrix, norm='ortho'."""
+    n = np.arange(n_mels, dtype=np.float64)
+    k = np.arange(n_mfcc, dtype=np.float64)[:, None]
+    dct = np.cos(np.pi / n_mels * (n + 0.5) * k)
+    dct[0] *= 1.0 / np.sqrt(2.0)
+    dct *= np.sqrt(2.0 / n_mels)
+    return dct.T
+
+
+def mfcc_torchaudio(x: np.ndarray) -> np.ndarray:
+    """B1..B5: (..., 16000) waveform -> (..., 13, 63) MFCC (coefficient-major)."""
+    p = power_spectrogram(preemphasis(x))               # (..., T, 257)
+    mel = p @ melscale_fbanks()                          # (..., T, 40)
+    logmel = np.log(mel + 1e-6)
+    mf = logmel @ create_dct()                           # (..., T, 13)
+    return np.swapaxes(mf, -1, -2)
+
+
+# --------------------------------------------------------------------------
+# B6: normalize_mfcc (extract_mfcc.py:47-88)
+# --------------------------------------------------------------------------
+def normalize_mfcc(m: np.ndarray, method: str = "cmvn") -> np.ndarray:
+    m = np.asarray(m, np.float64)
+    if method in ("standardization", "cmvn"):
+        mean = m.mean(axis=-1, keepdims=True)
+        std = m.std(axis=-1, ddof=1, keepdims=True)
+        std = np.where(std == 0, 1.0, std)
+        return (m - mean) / (std + 1e-8)
+    if method == "minmax":
+        mn = m.min(axis=-1, keepdims=True)
+        mx = m.max(axis=-1, keepdims=True)
+        return (m - mn) / (mx - mn + 1e-8)
+    return m
+
+
+def features_mode_b(x: np.ndarray) -> np.ndarray:
+    """Full mode-B front-end: waveform (..., 16000) -> CMVN'd (..., 13, 63)."""
+    return normalize_mfcc(mfcc_torchaudio(x), "cmvn")
+
+
+# --------------------------------------------------------------------------
+# CNN: LightweightKWS (wakeModel.py:4-34), NCW layout
+# --------------------------------------------------------------------------
+def _conv1d_k3p1(x: np.ndarray, w: np.ndarray) -> np.ndarray:
+    """x (B, Cin, T), w (Cout, Cin, 3) -> (B, Cout, T); padding=1, no bias."""
+    xp = np.pad(x, ((0, 0), (0, 0), (1, 1)))
+    T = x.shape[-1]
+    out = np.zeros((x.shape[0], w.shape[0], T))
+    for k in range(3):
+        out += np.einsum("oc,bct->bot", w[:, :, k], xp[:, :, k:k + T])
+    return out
+
+
+def _maxpool2(x: np.ndarray) -> np.ndarray:
+    T = x.shape[-1] // 2
+    return np.maximum(x[..., 0:2 * T:2], x[..., 1:2 * T:2])
+
+
+def kws_forward(feats: np.ndarray, w: dict) -> np.ndarray:
+    """feats (B, 13, 63) -> logits (B, 1).  ``w`` keys follow the reference
+    state dict: conv_layers.{0,3,6}.weight, classifier.{0,2}.weight."""
+    x = np.asarray(feats, np.float64)
+    for key in ("conv_layers.0.weight", "conv_layers.3.weight", "conv_layers.6.weight"):
+        x = _maxpool2(np.maximum(_conv1d_k3p1(x, np.asarray(w[key], np.float64)), 0.0))
+    g = x.mean(axis=-1)                                               # (B, 128)
+    h = np.maximum(g @ np.asarray(w["classifier.0.weight"], np.float64).T, 0.0)
+    return h @ np.asarray(w["classifier.2.weight"], np.float64).T      # (B, 1)
+
+
+def detect_mode_b(x: np.ndarray, w: dict) -> np.ndarray:
+    """Waveform (B, 16000) -> logits (B,)."""
+    return kws_forward(features_mode_b(x), w)[:, 0]
+
+
+# --------------------------------------------------------------------------
+# Synthetic clip generator -- host restatement of the
+# device generator in csrc/wk_synth.hip (same counter-based hash).
+# --------------------------------------------------------------------------
+def _mix32(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(16)
+    return x
+
+
+def synth_clips(seed: int, first: int, count: int, n: int = WIN_SAMPLES) -> np.ndarray:
+    """clamp(0.1*N(0,1), -1, 1) (+ 0.1*sin(2*pi*440*t/16000) on odd clips).
+
+    N(0,1) from Box-Muller over two 24-bit uniforms drawn from a counter hash
+    keyed on (seed, global clip index, sample index).  float32 output."""
+    clip = np.arange(first, first + count, dtype=np.uint64)[:, None]
+    s = np.arange(n, dtype=np.uint64)[None, :]
+    key = _mix32(np.uint64(seed) ^ (clip * np.uint64(0x9E3779B9)))
+    h1 = _mix32(key ^ (s * np.uint64(2) + np.uint64(0x68E31DA4)))
+    h2 = _mix32(h1 ^ np.uint64(0xB5297A4D))
+    u1 = ((h1 >> np.uint64(8)).astype(np.float32) + np.float32(1.0)) * np.float32(1.0 / 16777216.0)
+    u2 = (h2 >> np.uint64(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    r = np.sqrt(np.float32(-2.0) * np.log(u1))
+    g = (r * np.cos(np.float32(2.0 * np.pi) * u2)).astype(np.float32)
+    x = np.clip(np.float32(0.1) * g, -1.0, 1.0).astype(np.float32)
+    odd = (clip % np.uint64(2)) == 1
+    phase = ((s * np.uint64(440)) % np.uint64(16000)).astype(np.float32) * np.float32(1.0 / 16000.0)
+    sine = (np.float32(0.1) * np.sin(np.float32(2.0 * np.pi) * phase)).astype(np.float32)
+    return np.where(odd, x + sine, x).astype(np.float32)
