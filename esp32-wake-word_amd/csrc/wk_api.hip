@@ -272,6 +272,7 @@ void analyze_mfcc_range(float* mfcc, int size, const char* label) {
            sum / valid, valid, size);
   else
     fprintf(stderr, "E (MFCC) %s MFCC: No valid values\n", label ? label : "");
+  fflush(stdout);
 }
 
 }  // extern "C"

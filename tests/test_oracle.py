@@ -1,0 +1,110 @@
+"""CPU tests: the oracle against the committed golden vectors (no GPU)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import wk_oracle as O
+
+
+def test_onnx_weights_match_int8_kat_weights(golden_dir):
+    """xiaoa.info's int8 weights are round(w * 2^-exp) of xiaoa.onnx in esp-dl's
+    (N/16)WC16 layout: pins our ONNX reader and the weight layout exactly."""
+    from wakeword.onnx_reader import read_onnx
+    inits, ins, outs = read_onnx(os.path.join(golden_dir, "xiaoa.onnx"))
+    assert ins == ["input.1"] and outs == ["22"]
+    k = np.load(os.path.join(golden_dir, "kat.npz"))
+    for key, name in [("conv_layers_0_weight", "conv_layers.0.weight"), ("conv_layers_3_weight", "conv_layers.3.weight"),
+                      ("conv_layers_6_weight", "conv_layers.6.weight"), ("onnx__MatMul_23", "onnx::MatMul_23")]:
+        q = k["q_" + key].reshape(-1)
+        e = int(k["qexp_" + key])
+        w = inits[name]
+        if w.ndim == 3:
+            n, c, kk = w.shape
+            p = w.reshape(n // 16, 16, c, kk).transpose(0, 3, 2, 1).reshape(-1)
+        else:
+            kin, n = w.shape
+            p = w.T.reshape(n // 16, 16, kin).transpose(0, 2, 1).reshape(-1)
+        r = np.clip(np.round(p * 2.0 ** (-e)), -128, 127).astype(np.int64)
+        assert np.array_equal(r, q.astype(np.int64)), name
+
+
+def test_oracle_cnn_matches_reference_module(golden_dir, xiaoa_sd):
+    """Golden logits were produced by the reference's own LightweightKWS."""
+    s = np.load(os.path.join(golden_dir, "synth.npz"))
+    got = O.kws_forward(s["feats"], xiaoa_sd)[:, 0]
+    assert np.abs(got - s["logits"]).max() < 2e-5
+    g = np.load(os.path.join(golden_dir, "wavs.npz"))
+    got = O.kws_forward(g["feat_noise"], xiaoa_sd)[:, 0]
+    assert np.abs(got - g["logit_noise"]).max() < 2e-5
+
+
+def test_oracle_kat(golden_dir, xiaoa_sd):
+    k = np.load(os.path.join(golden_dir, "kat.npz"))
+    got = O.kws_forward(k["kat_feats"], xiaoa_sd)[0, 0]
+    assert abs(got - float(k["kat_ref_logit"][0])) < 2e-5
+    assert abs(got - (-5.0)) < 0.25          # int8 KAT -40 * 2^-3
+    # The KAT input is CMVN-like (per-coefficient mean ~0, std ~1): the CNN wants CMVN'd features.
+    f = k["kat_feats"][0]
+    assert np.abs(f.mean(axis=1)).max() < 0.2 and np.abs(f.std(axis=1, ddof=1) - 1).max() < 0.2
+
+
+def test_oracle_frontend_vs_torch_stft_restatement(golden_dir):
+    """Two independent restatements of the torchaudio front-end agree."""
+    g = np.load(os.path.join(golden_dir, "wavs.npz"))
+    assert np.abs(g["feat_zero"] - g["feat_zero_torch"]).max() < 1e-4
+    s = np.load(os.path.join(golden_dir, "synth.npz"))
+    assert np.abs(s["feats"] - s["feats_torch"]).max() < 1e-4
+
+
+def test_oracle_frontend_reproduces_golden(golden_dir):
+    g = np.load(os.path.join(golden_dir, "wavs.npz"))
+    got = O.features_mode_b(g["x_noise"])
+    assert np.abs(got - g["feat_noise"]).max() < 1e-5
+
+
+def test_torch_cpu_baseline_path(golden_dir, xiaoa_sd):
+    import torch
+    from oracle.wk_torch_cpu import TorchCpuPath
+    g = np.load(os.path.join(golden_dir, "wavs.npz"))
+    got = TorchCpuPath(xiaoa_sd)(torch.from_numpy(g["x_noise"])).numpy()
+    assert np.abs(got - g["logit_noise"]).max() < 1e-3
+
+
+def test_synth_generator_checksums(golden_dir):
+    s = np.load(os.path.join(golden_dir, "synth.npz"))
+    x = O.synth_clips(int(s["seed"]), int(s["first"]), int(s["count"]))
+    assert np.allclose(x.astype(np.float64).sum(axis=1), s["clip_checksum"], atol=1e-3)
+    assert x.dtype == np.float32 and x.shape == (16, 16000)
+    assert np.abs(x[0]).max() <= 1.0 and np.abs(x[1]).max() <= 1.1
+
+
+def test_wav_fixtures_match_golden_inputs(golden_dir):
+    """The committed WAVs (reference audio_data/flash) are the golden inputs."""
+    import wakeword.api as api
+    g = np.load(os.path.join(golden_dir, "wavs.npz"))
+    for name, xn in zip(g["name"], g["x_noise"]):
+        a = api.load_wav(os.path.join(golden_dir, "wav", str(name)))
+        n = min(len(a), 16000)
+        assert np.array_equal(xn[:n], a[:n])
+
+
+def test_melscale_nnz_and_edges():
+    fb = O.melscale_fbanks()
+    assert fb.shape == (257, 40)
+    assert int((fb > 1e-9).sum()) == 493
+    assert fb[0].sum() == 0 and fb[256].sum() < 1e-9
+
+
+def test_generated_mel_tables_match_oracle():
+    """The straight-line mel code in csrc/wk_tables.h carries fb/4 (mode B)."""
+    import re
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "esp32-wake-word_amd", "csrc", "wk_tables.h")).read()
+    fb = np.zeros((257, 40))
+    body = hdr.split("// melA:")[0]
+    for blk in re.finditer(r"\{ const float v = p\[(\d+)\];(.*?)\}", body):
+        k = int(blk.group(1))
+        for m in re.finditer(r"a(\d+) = __builtin_fmaf\(v, ([-0-9.e]+)f, a\d+\);", blk.group(2)):
+            fb[k, int(m.group(1))] += 4.0 * float(m.group(2))
+    ref = O.melscale_fbanks()
+    assert np.abs(fb - ref).max() < 1e-5   # torchaudio builds the bank in fp32
