@@ -7,9 +7,8 @@ namespace wk {
 
 constexpr int kWinSamples = 16000;   // 1 s @ 16 kHz (extract_mfcc.py:157)
 constexpr int kNFramesB = 63;        // 1 + 16000/256 with center=True
-constexpr int kPRow = 273;           // LDS pitch of one frame's power row (odd: lane-per-frame reads
-                                     // conflict-free; >=272 so the 16x17 transpose scratch fits)
-constexpr int kLRow = 41;            // LDS pitch of one log-mel row (odd)
+constexpr int kPRow = 271;           // LDS pitch of one frame's power row (odd: lane-per-frame reads
+                                     // conflict-free; >=271 so the 16x17 transpose scratch fits)
 constexpr int kFeBlock = 512;        // 8 waves per front-end workgroup
 
 struct cf {
@@ -88,11 +87,25 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops,
+// then s_barrier.  Unlike __syncthreads() it does not drain vmcnt, so global
+// loads issued as prefetch stay in flight across it.
+__device__ __forceinline__ void wg_barrier_lds() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
   return v;
 }
+
+__device__ __forceinline__ float to_f(float v) { return v; }
+__device__ __forceinline__ float to_f(int16_t v) { return (float)v * (1.0f / 32768.0f); }
 
 template <typename T> __device__ __forceinline__ float sample(const T* p, int64_t i);
 template <> __device__ __forceinline__ float sample<float>(const float* p, int64_t i) { return p[i]; }

@@ -62,44 +62,93 @@ __device__ __forceinline__ float pre_general(const T* __restrict__ x, int i, int
   return r > 0 ? __builtin_fmaf(-0.97f, xm, xr) : xr;
 }
 
-struct LaneConst {
-  float wr[10], wi[10];  // window at n = 32*n1 + 2j, +1
-  cf tw[16];             // W256^(j*k1)
-  cf w512;               // W512^j
+// Raw samples of one frame-group slot, prefetched into registers one round
+// ahead: x[i0], x[i0+1] for i0 = base + 32*n1 + 2j, plus x[base-1].  The
+// pre-emphasis partner x[i0-1] is the previous lane's x[i0+1] (DPP row
+// rotate), so it is not loaded twice.  Kept in the input type so the loads
+// stay outstanding until first use.
+template <typename T>
+struct Raw {
+  T x0[10], x1[10];
+  T xb;
+};
+
+template <typename T>
+__device__ __forceinline__ void load_raw(const T* __restrict__ x, int base, int j, bool act, Raw<T>& r) {
+  if (act) {
+#pragma unroll
+    for (int n1 = 0; n1 < 10; ++n1) {
+      const int i0 = base + 32 * n1 + 2 * j;
+      r.x0[n1] = x[i0];
+      r.x1[n1] = x[i0 + 1];
+    }
+    r.xb = x[base - 1];
+  }
+}
+
+__device__ __forceinline__ float row_ror1(float v) {  // lane l <- lane (l-1) mod 16 of its 16-lane row
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xF, 0xF, false));
+}
+
+// LDS tables shared by the workgroup.
+struct FeTables {
+  const float* win;   // [320] analysis window (mode-specific)
+  const float* tw;    // [15][16][2]: W256^(j*k1), k1 = 1..15
 };
 
 // One frame -> its power row (bins 0..256) in LDS, by one 16-lane group.
+// SLOW = general sample path (reflect padding / first-sample rule), used only
+// by the wave-rounds that hold the edge frames; it loads its own samples.
+// Stage 0: pre-emphasis + window of the 320 frame samples as 160 complex
+// (even, odd) pairs: lane j holds pair index 16*n1 + j, n1 = 0..9.
 template <bool MODE_B, bool SLOW, typename T>
-__device__ __forceinline__ void fe_frame(const T* __restrict__ x, int t, int n, int j, int lane,
-                                         float* __restrict__ row, const LaneConst& k, int esp_pack) {
-  cf a[16];
+__device__ __forceinline__ void fe_stage0(const T* __restrict__ x, const Raw<T>& raw, int t, int n, int j,
+                                          const FeTables& tb, cf (&a)[16]) {
   const int base = MODE_B ? (256 * t - 160) : (256 * t);
+  float prev_rot = 0.0f;
 #pragma unroll
   for (int n1 = 0; n1 < 10; ++n1) {
-    const int i0 = base + 32 * n1 + 2 * j;
     float y0, y1;
     if constexpr (!SLOW) {
-      const float xm = sample(x, i0 - 1), x0 = sample(x, i0), x1 = sample(x, i0 + 1);
+      const float x0 = to_f(raw.x0[n1]), x1 = to_f(raw.x1[n1]);
+      // x[i0-1]: lane j-1's x1 of this row; lane 0 takes lane 15's x1 of the previous row.
+      const float rot = row_ror1(x1);
+      const float xm = j != 0 ? rot : (n1 == 0 ? to_f(raw.xb) : prev_rot);
+      prev_rot = rot;
       y0 = __builtin_fmaf(-0.97f, xm, x0);
       y1 = __builtin_fmaf(-0.97f, x0, x1);
     } else {
+      const int i0 = base + 32 * n1 + 2 * j;
       y0 = pre_general<MODE_B>(x, i0, n);
       y1 = pre_general<MODE_B>(x, i0 + 1, n);
     }
-    a[n1] = {y0 * k.wr[n1], y1 * k.wi[n1]};
+    const float2 w = *reinterpret_cast<const float2*>(tb.win + 32 * n1 + 2 * j);
+    a[n1] = {y0 * w.x, y1 * w.y};
   }
 #pragma unroll
   for (int n1 = 10; n1 < 16; ++n1) a[n1] = {0.0f, 0.0f};
+}
 
+// Stages 1..4 of one frame -> its power row (bins 0..256) in LDS.
+template <bool MODE_B>
+__device__ __forceinline__ void fe_rest(cf (&a)[16], int j, int lane, float* __restrict__ row, const FeTables& tb,
+                                        cf w512, int esp_pack) {
   dft16(a);  // A[k1] at a[dft16_out(k1)]
 
-  // twiddle + 16x16 transpose through this frame's LDS row (pitch 17).
+  // twiddle W256^(j*k1) + 16x16 transpose through this frame's LDS row (pitch 17).
+  // (twiddles are applied in groups of 4 so their LDS reads do not all
+  // sit in VGPRs at once; re parts go straight to the transpose image.)
   cf b[16];
+  b[0] = a[0];
+  row[j] = b[0].re;
 #pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) b[k1] = k1 == 0 ? a[0] : cmul(a[dft16_out(k1)], k.tw[k1]);
+  for (int k1 = 1; k1 < 16; ++k1) {
+    const float2 w = *reinterpret_cast<const float2*>(tb.tw + ((k1 - 1) * 16 + j) * 2);
+    b[k1] = cmul(a[dft16_out(k1)], cf{w.x, w.y});
+    row[17 * k1 + j] = b[k1].re;
+    if ((k1 & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  }
   cf c[16];
-#pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) row[17 * k1 + j] = b[k1].re;
   wave_lds_sync();
 #pragma unroll
   for (int n2 = 0; n2 < 16; ++n2) c[n2].re = row[17 * j + n2];
@@ -113,28 +162,27 @@ __device__ __forceinline__ void fe_frame(const T* __restrict__ x, int t, int n, 
 
   dft16(c);  // Z[j + 16*k2] at c[dft16_out(k2)]
 
-  // Partner Z[256 - k]: lane (16-j)&15 of this group, register 15-k2; lane 0 uses its own.
-  const int src = ((lane & 48) | ((16 - j) & 15)) << 2;
-  cf zq[8];
-#pragma unroll
-  for (int k2 = 0; k2 < 8; ++k2) {
-    const cf s = c[dft16_out(15 - k2)];
-    const cf own = c[dft16_out((16 - k2) & 15)];
-    const float pr = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.re)));
-    const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.im)));
-    zq[k2] = j == 0 ? own : cf{pr, pi};
-  }
-  wave_lds_sync();
-
   // Real-FFT split: U = 2 V[k] = S - i*b, U' = conj(2 V[256-k]) = S + i*b with
   // S = Z[k] + conj Z[256-k], D = Z[k] - conj Z[256-k], b = W512^k D.
+  // Partner Z[256 - k]: lane (16-j)&15 of this group, register 15-k2 (ds_bpermute);
+  // lane 0 holds its own partner in register (16-k2)&15.
+  const int src = ((lane & 48) | ((16 - j) & 15)) << 2;
 #pragma unroll
   for (int k2 = 0; k2 <= 8; ++k2) {
     const cf zk = c[dft16_out(k2)];
-    const cf zq_ = k2 < 8 ? zq[k2] : c[dft16_out(8)];
+    cf zq_;
+    if (k2 < 8) {
+      const cf s = c[dft16_out(15 - k2)];
+      const cf own = c[dft16_out((16 - k2) & 15)];
+      const float pr = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.re)));
+      const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.im)));
+      zq_ = j == 0 ? own : cf{pr, pi};
+    } else {
+      zq_ = c[dft16_out(8)];
+    }
     const cf S = {zk.re + zq_.re, zk.im - zq_.im};
     const cf D = {zk.re - zq_.re, zk.im + zq_.im};
-    const cf tw = cmul(k.w512, w32(k2));
+    const cf tw = cmul(w512, w32(k2));
     const cf bb = cmul(tw, D);
     const float ur = S.re + bb.im, ui = S.im - bb.re;
     const float vr = S.re - bb.im, vi = S.im + bb.re;
@@ -188,67 +236,100 @@ __device__ __forceinline__ float cmvn_lane(float v, bool valid, int n) {
   return d / (sd + 1e-8f);
 }
 
+// LDS carve (floats): twiddles | window | log-mel [40][64] | power rows [63][271].
+constexpr int kTwOff = 0, kTwSize = 15 * 16 * 2;
+constexpr int kWinOff = kTwOff + kTwSize, kWinSize = 320;
+constexpr int kLOff = kWinOff + kWinSize, kLSize = 40 * WK_LSTRIDE;
+constexpr int kPOff = kLOff + kLSize, kPSize = kNFramesB * kPRow;
+constexpr int kFeLds = kPOff + kPSize;
+static_assert(kFeLds * 4 <= 81920, "front-end LDS must allow 2 workgroups per CU");
+
 template <bool MODE_B, typename T>
 __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __restrict__ audio, int64_t n_units,
                                                                   int n_chunks, int nf, int win_len,
                                                                   int64_t clip_stride, float* __restrict__ out,
                                                                   int esp_pack, int cmvn) {
-  __shared__ __attribute__((aligned(16))) float smem[kNFramesB * kPRow + 64 * kLRow];
-  float* P = smem;
-  float* L = smem + kNFramesB * kPRow;
+  __shared__ __attribute__((aligned(16))) float smem[kFeLds];
+  float* P = smem + kPOff;
+  float* L = smem + kLOff;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, j = lane & 15;
 
-  LaneConst k;
-#pragma unroll
-  for (int n1 = 0; n1 < 10; ++n1) {
-    const int nn = 32 * n1 + 2 * j;
-    k.wr[n1] = MODE_B ? kWinB[nn] : kWinA[nn];
-    k.wi[n1] = MODE_B ? kWinB[nn + 1] : kWinA[nn + 1];
+  for (int i = threadIdx.x; i < 320; i += kFeBlock) smem[kWinOff + i] = MODE_B ? kWinB[i] : kWinA[i];
+  for (int i = threadIdx.x; i < 15 * 16; i += kFeBlock) {
+    const int k1 = i / 16 + 1, jj = i % 16;
+    float sn, cs;
+    sincospif(-(float)(jj * k1) / 128.0f, &sn, &cs);
+    smem[kTwOff + 2 * i] = cs;
+    smem[kTwOff + 2 * i + 1] = sn;
   }
-#pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) {
-    float s, cc;
-    sincospif(-(float)(j * k1) / 128.0f, &s, &cc);
-    k.tw[k1] = {cc, s};
-  }
+  const FeTables tb = {smem + kWinOff, smem + kTwOff};
+  cf w512;
   {
-    float s, cc;
-    sincospif(-(float)j / 256.0f, &s, &cc);
-    k.w512 = {cc, s};
+    float sn, cs;
+    sincospif(-(float)j / 256.0f, &sn, &cs);
+    w512 = {cs, sn};
   }
   // Frame slots: groups 0/1 (and 2/3) of a wave take frames 16 apart so their
   // pitch-17 transpose images fall in disjoint LDS banks.
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);
+  __syncthreads();
+
+  // Wave-round (unit u, round r) geometry: frame t (within the clip), local
+  // frame fl (within the 63-frame chunk), frames in the chunk, edge flag.
+  auto frame_of = [&](int64_t u, int r, int& t, int& fl, int& nfc, bool& slow, const T*& xp) {
+    const int64_t clip = MODE_B ? u : u / n_chunks;   // mode B: one chunk per clip
+    const int chunk = (int)(u - clip * n_chunks);
+    xp = audio + clip * clip_stride;
+    const int f0 = chunk * kNFramesB;
+    nfc = min(kNFramesB, nf - f0);
+    fl = wave + 8 * r + slot_base;
+    t = f0 + fl;
+    slow = MODE_B ? ((r == 0 && wave == 0) || (r == 1 && wave == 6)) : (chunk == 0 && r == 0 && wave == 0);
+  };
+  auto prefetch = [&](int64_t u, int r, Raw<T>& dst) {
+    if (u < n_units) {
+      int t, fl, nfc;
+      bool slow;
+      const T* xp;
+      frame_of(u, r, t, fl, nfc, slow, xp);
+      if (!slow) load_raw(xp, MODE_B ? 256 * t - 160 : 256 * t, j, fl < nfc, dst);
+    }
+  };
+
+  Raw<T> pf;
+  prefetch(blockIdx.x, 0, pf);
 
   for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
-    const int64_t clip = u / n_chunks;
+    const int64_t clip = MODE_B ? u : u / n_chunks;
     const int chunk = (int)(u - clip * n_chunks);
-    const T* x = audio + clip * clip_stride;
     const int f0 = chunk * kNFramesB;
     const int nfc = min(kNFramesB, nf - f0);
 
-#pragma unroll
+#pragma unroll 1
     for (int r = 0; r < 2; ++r) {
-      const int fl = wave + 8 * r + slot_base;
-      const int t = f0 + fl;
-      const bool slow = MODE_B ? ((r == 0 && wave == 0) || (r == 1 && wave == 6))
-                               : (chunk == 0 && r == 0 && wave == 0);
+      int t, fl, nfc_r;
+      bool slow;
+      const T* xp;
+      frame_of(u, r, t, fl, nfc_r, slow, xp);
+      cf a[16];
       if (fl < nfc) {
-        float* row = P + fl * kPRow;
         if (slow)
-          fe_frame<MODE_B, true>(x, t, win_len, j, lane, row, k, esp_pack);
+          fe_stage0<MODE_B, true>(xp, pf, t, win_len, j, tb, a);
         else
-          fe_frame<MODE_B, false>(x, t, win_len, j, lane, row, k, esp_pack);
+          fe_stage0<MODE_B, false>(xp, pf, t, win_len, j, tb, a);
       }
+      // pf is consumed: prefetch the next wave-round, (u,1) or (u+grid,0), into it.
+      prefetch(r == 0 ? u : u + gridDim.x, r ^ 1, pf);
+      if (fl < nfc) fe_rest<MODE_B>(a, j, lane, P + fl * kPRow, tb, w512, esp_pack);
     }
-    __syncthreads();
+    wg_barrier_lds();
 
-    mel_dispatch<MODE_B>(wave, P + min(lane, nfc - 1) * kPRow, L + lane * kLRow);
-    __syncthreads();
+    mel_dispatch<MODE_B>(wave, P + min(lane, nfc - 1) * kPRow, L + lane);
+    wg_barrier_lds();
 
-    const float* lrow = L + lane * kLRow;
+    const float* lrow = L + lane;
     const bool valid = lane < nfc;
     const int c0 = wave < 5 ? 2 * wave : wave + 5;
     const int nc = wave < 5 ? 2 : 1;

@@ -166,9 +166,9 @@ def emit_mel(fb: np.ndarray, name: str, mode: str, scale: float):
                                  for m, wt in terms) + " }")
         for m in range(a, b):
             if mode == "B":
-                lines.append(f"  l[{m}] = logf(a{m} + 1e-6f);")
+                lines.append(f"  l[{m} * WK_LSTRIDE] = logf(a{m} + 1e-6f);")
             else:
-                lines.append(f"  l[{m}] = logf(__builtin_fmaxf(a{m}, 1e-12f));")
+                lines.append(f"  l[{m} * WK_LSTRIDE] = logf(__builtin_fmaxf(a{m}, 1e-12f));")
         lines.append("}")
     lines.append(f"template <int W> __device__ __forceinline__ void {name}_wave(const float* p, float* l);")
     for w in range(N_WAVES):
@@ -185,7 +185,7 @@ def main():
     wA = window_mode_a()
     out = ["// GENERATED by esp32-wake-word_amd/tools/gen_tables.py -- do not edit.",
            "// Constants restated from torchaudio (mode B) and main/esp_mfcc/mfcc.c (mode A).",
-           "#pragma once", ""]
+           "#pragma once", "", "#ifndef WK_LSTRIDE", "#define WK_LSTRIDE 64  // log-mel image is [mel][frame]", "#endif", ""]
     out.append(f"// nnz(mode B fbank) = {int((fbB != 0).sum())}, nnz(mode A fbank) = {int((fbA != 0).sum())}")
     out.append("__constant__ float kWinB[320] = {" + ", ".join(f32(v) for v in wB) + "};")
     out.append("__constant__ float kWinA[320] = {" + ", ".join(f32(v) for v in wA) + "};")
@@ -197,11 +197,11 @@ def main():
     out.append(emit_mel(fbA, "melA", "A", 1.0))
     out.append("")
     for c in range(N_MFCC):
-        body = " ".join(f"s = __builtin_fmaf(l[{m}], {f32(dB[c, m])}, s);" for m in range(N_MELS))
+        body = " ".join(f"s = __builtin_fmaf(l[{m} * WK_LSTRIDE], {f32(dB[c, m])}, s);" for m in range(N_MELS))
         out.append(f"__device__ __forceinline__ float dctB_{c}(const float* __restrict__ l) {{ float s = 0.0f; {body} return s; }}")
     for c in range(N_MFCC):
         scale = math.sqrt(1.0 / N_MELS) if c == 0 else math.sqrt(2.0 / N_MELS)
-        body = " ".join(f"s = __builtin_fmaf(l[{m}], {f32(dA[c, m])}, s);" for m in range(N_MELS))
+        body = " ".join(f"s = __builtin_fmaf(l[{m} * WK_LSTRIDE], {f32(dA[c, m])}, s);" for m in range(N_MELS))
         out.append(f"__device__ __forceinline__ float dctA_{c}(const float* __restrict__ l) {{ float s = 0.0f; {body} return {f32(scale)} * s; }}")
     out.append("template <bool MODE_B> __device__ __forceinline__ float dct_coef(int c, const float* __restrict__ l) {")
     out.append("  switch (c) {")

@@ -24,7 +24,7 @@ OBJDIR = os.path.join(ROOT, "build")
 SOURCES = ["wk_frontend.hip", "wk_cnn.hip", "wk_misc.hip", "wk_api.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WK_OFFLOAD_ARCH", "gfx950")
-CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-fno-signed-zeros", "-ffp-contract=fast",
+CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-fno-signed-zeros", "-ffp-contract=fast", "-fno-slp-vectorize",
           "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", CSRC]
 
 
