@@ -5,6 +5,7 @@
 #include <math.h>
 
 #include <mutex>
+#include <vector>
 #include <string>
 
 #include "wakeword.h"
@@ -14,8 +15,10 @@ struct wk_handle {
   wk_config cfg;
   int n_cu;
   float* d_weights;      // packed WK_NUM_WEIGHTS floats, or nullptr (front-end only handle)
+  float* d_packed;       // fragment-major weights (wk::pack_fragments) for the fused kernel
   float* d_feats_ws;     // feature workspace for the unfused path
   int64_t ws_clips;
+  int unfused;           // WAKEWORD_UNFUSED=1: front-end + CNN as two kernels (A/B testing)
 };
 
 namespace {
@@ -77,6 +80,10 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
   wk_handle* h = (wk_handle*)calloc(1, sizeof(wk_handle));
   if (!h) return WK_ERR_NO_MEMORY;
   h->cfg = *cfg;
+  {
+    const char* u = getenv("WAKEWORD_UNFUSED");
+    h->unfused = u && u[0] == '1';
+  }
   wk_status st = on_device(cfg->device, [&]() -> wk_status {
     hipDeviceProp_t prop;
     hipError_t e2 = hipGetDeviceProperties(&prop, cfg->device);
@@ -88,6 +95,13 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
       if ((e2 = hipMemcpy(h->d_weights, host_weights, sizeof(float) * WK_NUM_WEIGHTS, hipMemcpyHostToDevice)) !=
           hipSuccess)
         return hip_fail(e2, "hipMemcpy(weights)");
+      std::vector<float> pk(wk::kNumPacked);
+      wk::pack_fragments(host_weights, pk.data());
+      if ((e2 = hipMalloc(&h->d_packed, sizeof(float) * wk::kNumPacked)) != hipSuccess)
+        return hip_fail(e2, "hipMalloc(packed weights)");
+      if ((e2 = hipMemcpy(h->d_packed, pk.data(), sizeof(float) * wk::kNumPacked, hipMemcpyHostToDevice)) !=
+          hipSuccess)
+        return hip_fail(e2, "hipMemcpy(packed weights)");
       h->ws_clips = kWorkspaceClips;
       if ((e2 = hipMalloc(&h->d_feats_ws, sizeof(float) * 13 * 63 * h->ws_clips)) != hipSuccess)
         return hip_fail(e2, "hipMalloc(workspace)");
@@ -107,6 +121,7 @@ wk_status wk_destroy(wk_handle* h) {
   on_device(h->cfg.device, [&]() -> wk_status {
     if (h->d_weights) (void)hipFree(h->d_weights);
     if (h->d_feats_ws) (void)hipFree(h->d_feats_ws);
+    if (h->d_packed) (void)hipFree(h->d_packed);
     return WK_OK;
   });
   free(h);
@@ -168,6 +183,11 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
     return WK_ERR_UNSUPPORTED;
   }
   return on_device(h->cfg.device, [&]() -> wk_status {
+    if (!h->unfused) {
+      hipError_t e = wk::launch_fused(dtype == WK_DTYPE_I16, d_audio, batch, clip_stride, h->d_packed, d_logits,
+                                      d_feats_or_null, h->n_cu, (hipStream_t)stream);
+      return e == hipSuccess ? WK_OK : hip_fail(e, "fused launch");
+    }
     const size_t esz = dtype == WK_DTYPE_I16 ? 2 : 4;
     for (int64_t c0 = 0; c0 < batch; c0 += h->ws_clips) {
       const int64_t n = batch - c0 < h->ws_clips ? batch - c0 : h->ws_clips;

@@ -1,0 +1,68 @@
+// wk_cnn_dev.h -- device helpers of the xiaoa CNN on fp32 MFMA (shared by
+// wk_cnn.hip and wk_fused.hip).  See wk_cnn.hip for the design notes.
+#pragma once
+#include "wk_common.h"
+
+namespace wk {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float swap_adjacent(float v) {  // lane l <- lane l^1
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+
+// Two N-tiles (16 time columns each) of one conv layer, sharing the A fragments.
+// boff = lane part + clip*CLIP + t0; step s covers k = 4s..4s+3 = (tap, ci0..ci0+3).
+// CHUNK > 0 fences the instruction stream every CHUNK steps so the B-fragment
+// LDS reads are not all hoisted ahead of the MFMAs (VGPR budget of the fused
+// kernel); CHUNK = 0 leaves scheduling to the compiler.
+template <int NSTEP, int CIP, int SPT, int CHUNK = 0>
+__device__ __forceinline__ void conv_pair(const float* __restrict__ act, const float (&wf)[NSTEP], int boff_a,
+                                          int boff_b, f32x4& acc_a, f32x4& acc_b) {
+#pragma unroll
+  for (int s = 0; s < NSTEP; ++s) {
+    const int off = (s % SPT) * 4 * CIP + s / SPT;
+    acc_a = mfma4(wf[s], act[boff_a + off], acc_a);
+    acc_b = mfma4(wf[s], act[boff_b + off], acc_b);
+    if (CHUNK > 0 && (s % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ReLU -> maxpool(2) -> store the pooled row into the next layer's image.
+template <int CIP_N, int CLIP_N, int TN>
+__device__ __forceinline__ void epi_pool(const f32x4& acc, float* __restrict__ next, int co0, int clip, int t0,
+                                         int lane) {
+  const int t = t0 + (lane & 15);
+  const int tp = t >> 1;
+  const bool w = !(lane & 1) && tp < TN;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = fmaxf(acc[r], 0.0f);
+    v = fmaxf(v, swap_adjacent(v));
+    if (w) next[(co0 + 4 * (lane >> 4) + r) * CIP_N + clip * CLIP_N + 1 + tp] = v;
+  }
+}
+
+// ReLU -> maxpool(2) (15 -> 7, floor) -> mean over the 7 pooled steps.
+template <int GSTRIDE>
+__device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g, int co0, int clip, int lane) {
+  const int tt = lane & 15;
+  const bool w = !(lane & 1) && tt <= 12;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = fmaxf(acc[r], 0.0f);
+    v = fmaxf(v, swap_adjacent(v));
+    float s = w ? v : 0.0f;
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    s += __shfl_xor(s, 8, 64);
+    if (tt == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s / 7.0f;
+  }
+}
+
+}  // namespace wk

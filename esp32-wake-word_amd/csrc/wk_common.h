@@ -104,6 +104,15 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Buffer-resource loads: base in SGPRs, per-lane byte offset in one VGPR, a
+// wave-uniform byte offset in an SGPR -- no 64-bit VGPR address per load.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float buf_load(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
 __device__ __forceinline__ float to_f(float v) { return v; }
 __device__ __forceinline__ float to_f(int16_t v) { return (float)v * (1.0f / 32768.0f); }
 

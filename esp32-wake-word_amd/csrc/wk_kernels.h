@@ -33,4 +33,45 @@ constexpr int kOffF1 = kOffW3 + 128 * 64 * 3;   // classifier.0.weight [64][128]
 constexpr int kOffF2 = kOffF1 + 64 * 128;       // classifier.2.weight [1][64]
 constexpr int kNumWeights = kOffF2 + 64;        // 40224
 
+// Fragment-major copy of the weights for the MFMA kernels: for each 16-row
+// output tile and k-step s (k = 4s..4s+3), the 64 values lane l feeds as the
+// A operand of v_mfma_f32_16x16x4_f32 (row = l&15, k = 4s + (l>>4)), so a
+// wave loads one fragment with one coalesced 256-byte load.
+//   conv k order: k = tap*Cin_pad + ci  (Cin_pad = 16 for conv1, zero rows)
+constexpr int kPkW1 = 0;                        // [2 tiles][12 s][64]
+constexpr int kPkW2 = kPkW1 + 2 * 12 * 64;      // [4][24][64]
+constexpr int kPkW3 = kPkW2 + 4 * 24 * 64;      // [8][48][64]
+constexpr int kPkF1 = kPkW3 + 8 * 48 * 64;      // [4 o-tiles][32 s][64]  (k = 4s + lane>>4)
+constexpr int kPkF2 = kPkF1 + 4 * 32 * 64;      // [64]
+constexpr int kNumPacked = kPkF2 + 64;
+
+// Host-side packing of the WK_NUM_WEIGHTS blob into the fragment-major layout.
+inline void pack_fragments(const float* w, float* pk) {
+  for (int t = 0; t < 2; ++t)
+    for (int s = 0; s < 12; ++s)
+      for (int l = 0; l < 64; ++l) {
+        const int co = 16 * t + (l & 15), ci = 4 * (s & 3) + (l >> 4), tap = s >> 2;
+        pk[kPkW1 + (t * 12 + s) * 64 + l] = ci < 13 ? w[kOffW1 + (co * 13 + ci) * 3 + tap] : 0.0f;
+      }
+  for (int t = 0; t < 4; ++t)
+    for (int s = 0; s < 24; ++s)
+      for (int l = 0; l < 64; ++l) {
+        const int co = 16 * t + (l & 15), ci = 4 * (s & 7) + (l >> 4), tap = s >> 3;
+        pk[kPkW2 + (t * 24 + s) * 64 + l] = w[kOffW2 + (co * 32 + ci) * 3 + tap];
+      }
+  for (int t = 0; t < 8; ++t)
+    for (int s = 0; s < 48; ++s)
+      for (int l = 0; l < 64; ++l) {
+        const int co = 16 * t + (l & 15), ci = 4 * (s & 15) + (l >> 4), tap = s >> 4;
+        pk[kPkW3 + (t * 48 + s) * 64 + l] = w[kOffW3 + (co * 64 + ci) * 3 + tap];
+      }
+  for (int t = 0; t < 4; ++t)
+    for (int s = 0; s < 32; ++s)
+      for (int l = 0; l < 64; ++l) {
+        const int o = 16 * t + (l & 15), c = 4 * s + (l >> 4);
+        pk[kPkF1 + (t * 32 + s) * 64 + l] = w[kOffF1 + o * 128 + c];
+      }
+  for (int o = 0; o < 64; ++o) pk[kPkF2 + o] = w[kOffF2 + o];
+}
+
 }  // namespace wk

@@ -21,7 +21,7 @@ CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(PKG, "libwakeword.so")
 OBJDIR = os.path.join(ROOT, "build")
-SOURCES = ["wk_frontend.hip", "wk_cnn.hip", "wk_misc.hip", "wk_api.hip"]
+SOURCES = ["wk_frontend.hip", "wk_cnn.hip", "wk_fused.hip", "wk_misc.hip", "wk_api.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WK_OFFLOAD_ARCH", "gfx950")
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-fno-signed-zeros", "-ffp-contract=fast", "-fno-slp-vectorize",

@@ -54,3 +54,80 @@ def test_end_to_end_wavs(model, golden_dir):
     g = np.load(os.path.join(golden_dir, "wavs.npz"))
     got = model.detect(g["x_noise"]).cpu().numpy()
     assert np.abs(got - g["logit_noise"]).max() < LOGIT_ATOL
+
+
+def _unfused_model(golden_dir):
+    import wakeword
+    os.environ["WAKEWORD_UNFUSED"] = "1"
+    try:
+        return wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"))
+    finally:
+        del os.environ["WAKEWORD_UNFUSED"]
+
+
+def test_fused_matches_unfused_and_oracle(model, golden_dir):
+    """The warp-specialised fused kernel vs the two-kernel path vs the oracle."""
+    x = O.synth_clips(1234, 100, 40)
+    lf, ff = model.detect(x, return_features=True)
+    lu, fu = _unfused_model(golden_dir).detect(x, return_features=True)
+    lf, ff, lu, fu = (t.cpu().numpy() for t in (lf, ff, lu, fu))
+    assert np.abs(ff - fu).max() < 1e-5
+    assert np.abs(lf - lu).max() < 1e-5
+    ref = O.kws_forward(O.features_mode_b(x), model.state_dict())[:, 0]
+    assert np.abs(lf - ref).max() < LOGIT_ATOL
+
+
+@pytest.mark.parametrize("n", [1, 3, 5, 17, 300])
+def test_ragged_batches(model, n):
+    """Batch sizes that leave partial CNN batches / idle workgroups."""
+    x = O.synth_clips(99, 7, n)
+    got = model.detect(x).cpu().numpy()
+    ref = O.kws_forward(O.features_mode_b(x), model.state_dict())[:, 0]
+    assert got.shape == (n,) and np.abs(got - ref).max() < LOGIT_ATOL
+
+
+def test_int16_input_equals_scaled_float(model):
+    rng = np.random.default_rng(5)
+    xi = (rng.standard_normal((12, 16000)) * 3000).clip(-32768, 32767).astype(np.int16)
+    a = model.detect(xi).cpu().numpy()
+    b = model.detect(xi.astype(np.float32) / 32768.0).cpu().numpy()
+    assert np.array_equal(a, b)
+
+
+def test_deterministic_and_batch_invariant(model):
+    import wakeword
+    x = wakeword.synth_clips(1234, 0, 2048)
+    a = model.detect(x).cpu().numpy()
+    b = model.detect(x).cpu().numpy()
+    assert np.array_equal(a, b)
+    c = model.detect(x[1000:1100]).cpu().numpy()
+    assert np.array_equal(a[1000:1100], c)
+
+
+def test_device_generator_matches_host(gpu):
+    import wakeword
+    d = wakeword.synth_clips(1234, 3, 5).cpu().numpy()
+    h = O.synth_clips(1234, 3, 5)
+    assert np.abs(d - h).max() < 1e-5
+
+
+def test_full_size_batch_sample_parity(model):
+    """BASELINE config 2 size (65,536 clips): every logit finite, a spread
+    sample of clips matches the oracle."""
+    import wakeword
+    B = 65536
+    x = wakeword.synth_clips(1234, 0, B)
+    got = model.detect(x).cpu().numpy()
+    assert np.isfinite(got).all()
+    idx = np.linspace(0, B - 1, 24).astype(int)
+    xs = x[idx].cpu().numpy()
+    ref = O.kws_forward(O.features_mode_b(xs), model.state_dict())[:, 0]
+    assert np.abs(got[idx] - ref).max() < LOGIT_ATOL
+
+
+def test_error_paths(model):
+    import wakeword
+    with pytest.raises(wakeword.WakewordError):
+        model.detect(np.zeros((2, 8000), np.float32))     # mode B needs 16000-sample windows
+    out = model.detect(np.zeros((0, 16000), np.float32))
+    assert out.shape == (0,)
