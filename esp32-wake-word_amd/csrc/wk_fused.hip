@@ -39,36 +39,45 @@ constexpr int kCtrlOff = kFcpOff + 2 * 64 * NBF;    // control words
 constexpr int kFusedLds = kCtrlOff + 16;
 static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 
-enum { kCtrlFeBar = 0, kCtrlCnnBar = 1, kCtrlFeatReady = 2, kCtrlAct0Free = 3 };
+enum { kCtrlFeBar = 0, kCtrlCnnBar = 1, kCtrlFeatReady = 2, kCtrlAct0Free = 3, kCtrlAbort = 15 };
+// Every spin is bounded (~4M sleeps, well under a second): a protocol bug
+// yields wrong logits and a drained grid, never a hung GPU.
+constexpr unsigned kSpinLimit = 1u << 22;
 
 __device__ __forceinline__ unsigned lds_load(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Spin until ctrl[idx] >= v.  On a timeout the workgroup's abort word is set
+// and every later spin returns at once.
+__device__ __forceinline__ void spin_until(unsigned* ctrl, int idx, unsigned v) {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  for (unsigned n = 0; lds_load(ctrl + idx) < v; ++n) {
+    if (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort)) {
+      __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 // Barrier among the 8 waves of one role (LDS counter; s_barrier would also
 // stop the other role's waves).  LDS operations of a wave complete in order,
 // so a wave's data writes are visible before its arrival is.
-__device__ __forceinline__ void role_sync(unsigned* ctr, unsigned& gen, int lane) {
+__device__ __forceinline__ void role_sync(unsigned* ctrl, int idx, unsigned& gen, int lane) {
   gen += 8;
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  while (lds_load(ctr) < gen) __builtin_amdgcn_s_sleep(1);
-  asm volatile("" ::: "memory");
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  if (lane == 0) __hip_atomic_fetch_add(ctrl + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  spin_until(ctrl, idx, gen);
 }
 
-__device__ __forceinline__ void wait_at_least(const unsigned* p, unsigned v) {
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  while (lds_load(p) < v) __builtin_amdgcn_s_sleep(2);
-  asm volatile("" ::: "memory");
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-__device__ __forceinline__ void signal_add(unsigned* p, int lane) {
+__device__ __forceinline__ void signal_add(unsigned* ctrl, int idx, int lane) {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (lane == 0) __hip_atomic_fetch_add(ctrl + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
@@ -117,14 +126,14 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       prefetch(r == 0 ? i : i + 1, r ^ 1, pf);
       if (fl < kNFramesB) fe_rest<true>(a, j, lane, P + fl * kPRow, tb, w512, 0);
     }
-    role_sync(ctrl + kCtrlFeBar, gen, lane);
+    role_sync(ctrl, kCtrlFeBar, gen, lane);
 
     mel_dispatch<true>(wave, P + min(lane, kNFramesB - 1) * kPRow, L + lane);
-    role_sync(ctrl + kCtrlFeBar, gen, lane);
+    role_sync(ctrl, kCtrlFeBar, gen, lane);
 
     const int64_t b = i / NBF;
     const int s = (int)(i - b * NBF);
-    if (s == 0 && b > 0) wait_at_least(ctrl + kCtrlAct0Free, (unsigned)b);   // CNN done reading batch b-1
+    if (s == 0 && b > 0) spin_until(ctrl, kCtrlAct0Free, (unsigned)b);   // CNN done reading batch b-1
     const float* lrow = L + lane;
     const bool valid = lane < kNFramesB;
     const int c0 = wave < 5 ? 2 * wave : wave + 5;
@@ -137,7 +146,7 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
         if (feats_out) feats_out[clip * (13 * kNFramesB) + cc * kNFramesB + lane] = y;
       }
     }
-    if (s == NBF - 1 || i == n_mine - 1) signal_add(ctrl + kCtrlFeatReady, lane);
+    if (s == NBF - 1 || i == n_mine - 1) signal_add(ctrl, kCtrlFeatReady, lane);
   }
 }
 
@@ -173,7 +182,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 #pragma unroll
       for (int s = 0; s < 12; ++s) w1[s] = buf_load(rs, lv, 4 * (kPkW1 + ((cw & 1) * 12 + s) * 64));
     }
-    wait_at_least(ctrl + kCtrlFeatReady, 8u * (unsigned)(b + 1));
+    spin_until(ctrl, kCtrlFeatReady, 8u * (unsigned)(b + 1));
 
     // conv1: co tile (cw&1), clip (cw>>1), 4 t-tiles.
     {
@@ -188,8 +197,8 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         epi_pool<F1_CI, F1_CLIP, 31>(acc_b, F1, co0, cl, tb, lane);
       }
     }
-    role_sync(ctrl + kCtrlCnnBar, gen, lane);
-    if (cw == 0) signal_add(ctrl + kCtrlAct0Free, lane);   // front-end may overwrite the conv1 image
+    role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    if (cw == 0) signal_add(ctrl, kCtrlAct0Free, lane);   // front-end may overwrite the conv1 image
 
     // conv2: co tile (cw&3), clips 2*(cw>>2) + {0,1}, 2 t-tiles each.
     {
@@ -207,7 +216,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         epi_pool<F2_CI, F2_CLIP, 15>(acc_b, F2, co0, cl, 16, lane);
       }
     }
-    role_sync(ctrl + kCtrlCnnBar, gen, lane);
+    role_sync(ctrl, kCtrlCnnBar, gen, lane);
 
     // conv3: co tile cw, the 4 clips; GAP -> G[128][4].
     {
@@ -227,7 +236,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 #pragma unroll
       for (int s = 0; s < 16; ++s) wf1[s] = buf_load(rs, lv, 4 * (kPkF1 + ((cw & 3) * 32 + 16 * (cw >> 2) + s) * 64));
     }
-    role_sync(ctrl + kCtrlCnnBar, gen, lane);
+    role_sync(ctrl, kCtrlCnnBar, gen, lane);
 
     // classifier.0 (128 -> 64): o tile (cw&3), k half (cw>>2); columns >= NBF are don't-care.
     {
@@ -240,7 +249,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         for (int r = 0; r < 4; ++r) FCP[kh * 64 * NBF + (16 * (cw & 3) + 4 * lk + r) * NBF + li] = acc[r];
       }
     }
-    role_sync(ctrl + kCtrlCnnBar, gen, lane);
+    role_sync(ctrl, kCtrlCnnBar, gen, lane);
 
     // ReLU -> classifier.2 (64 -> 1): lane = (o group q = lane>>2, clip = lane&3).
     if (cw == 0) {
