@@ -22,47 +22,66 @@ __device__ __forceinline__ cf w32(int k2) {
   }
 }
 
-// Pre-emphasised sample at (centred) index i, general path.
-//   mode B: reflect padding of the pre-emphasised signal (torch.stft center).
-//   mode A: no padding; y[0] = x[0] (mfcc.c:70).
-template <bool MODE_B, typename T>
-__device__ __forceinline__ float pre_general(const T* __restrict__ x, int i, int n) {
-  int r = i;
-  if (MODE_B) {
-    r = r < 0 ? -r : r;
-    r = r > n - 1 ? 2 * (n - 1) - r : r;
-  }
-  const float xr = sample(x, r);
-  const float xm = sample(x, r > 0 ? r - 1 : 0);
-  return r > 0 ? __builtin_fmaf(-0.97f, xm, xr) : xr;
-}
-
 // Raw samples of one frame-group slot, prefetched into registers one round
-// ahead: x[i0], x[i0+1] for i0 = base + 32*n1 + 2j, plus x[base-1].  The
-// pre-emphasis partner x[i0-1] is the previous lane's x[i0+1] (DPP row
-// rotate), so it is not loaded twice.  Kept in the input type so the loads
-// stay outstanding until first use.
+// ahead (buffer loads: clip base in SGPRs, out-of-range reads return 0):
+// x0[n1] = x[r(i0)], x1[n1] = x[r(i0+1)] for i0 = base + 32*n1 + 2j, with
+// r() the reflection of torch.stft's centre padding (mode B) -- identity
+// except on the two edge frames.  The pre-emphasis partner of each sample is
+// a neighbouring lane's value (DPP row rotate), so it is not loaded twice;
+// xb covers the one partner outside the slot (lane 0: x[r(base-1)], lane 15:
+// x[r(i0(9,15)+2)]).  Kept in the input type so the loads stay outstanding
+// until first use.
 template <typename T>
 struct Raw {
   T x0[10], x1[10];
   T xb;
 };
 
-template <typename T>
-__device__ __forceinline__ void load_raw(const T* __restrict__ x, int base, int j, bool act, Raw<T>& r) {
-  if (act) {
+template <typename T> __device__ __forceinline__ T raw_ld(__amdgpu_buffer_rsrc_t r, int idx);
+template <> __device__ __forceinline__ float raw_ld<float>(__amdgpu_buffer_rsrc_t r, int idx) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, idx * 4, 0, 0));
+}
+template <> __device__ __forceinline__ int16_t raw_ld<int16_t>(__amdgpu_buffer_rsrc_t r, int idx) {
+  return (int16_t)__builtin_amdgcn_raw_buffer_load_b16(r, idx * 2, 0, 0);
+}
+
+// Reflect index i of the centred (padded) signal of length n into [0, n).
+__device__ __forceinline__ int refl_idx(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i > n - 1 ? 2 * (n - 1) - i : i;
+}
+
+// GENERAL (wave-uniform) = this wave-round holds an edge frame: per-lane
+// reflected indices.  Otherwise the 21 loads share one offset VGPR.
+template <bool MODE_B, typename T>
+__device__ __forceinline__ void load_raw(__amdgpu_buffer_rsrc_t rs, int base, int j, int n, bool act, bool general,
+                                         Raw<T>& r) {
+  if (!act) return;
+  if (!general) {
+    const int v0 = base + 2 * j;
+#pragma unroll
+    for (int n1 = 0; n1 < 10; ++n1) {
+      r.x0[n1] = raw_ld<T>(rs, v0 + 32 * n1);
+      r.x1[n1] = raw_ld<T>(rs, v0 + 32 * n1 + 1);
+    }
+    r.xb = raw_ld<T>(rs, base - 1);   // mode A frame 0: index -1 -> 0 (y[0] = x[0], mfcc.c:70)
+  } else {
 #pragma unroll
     for (int n1 = 0; n1 < 10; ++n1) {
       const int i0 = base + 32 * n1 + 2 * j;
-      r.x0[n1] = x[i0];
-      r.x1[n1] = x[i0 + 1];
+      r.x0[n1] = raw_ld<T>(rs, MODE_B ? refl_idx(i0, n) : i0);
+      r.x1[n1] = raw_ld<T>(rs, MODE_B ? refl_idx(i0 + 1, n) : i0 + 1);
     }
-    r.xb = x[base - 1];
+    const int ib = j == 15 ? base + 32 * 9 + 32 : base - 1;
+    r.xb = raw_ld<T>(rs, MODE_B ? refl_idx(ib, n) : ib);
   }
 }
 
 __device__ __forceinline__ float row_ror1(float v) {  // lane l <- lane (l-1) mod 16 of its 16-lane row
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_rol1(float v) {  // lane l <- lane (l+1) mod 16 of its 16-lane row
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x12F, 0xF, 0xF, false));
 }
 
 // LDS tables shared by the workgroup.
@@ -71,31 +90,34 @@ struct FeTables {
   const float* tw;    // [15][16][2]: W256^(j*k1), k1 = 1..15
 };
 
-// One frame -> its power row (bins 0..256) in LDS, by one 16-lane group.
-// SLOW = general sample path (reflect padding / first-sample rule), used only
-// by the wave-rounds that hold the edge frames; it loads its own samples.
 // Stage 0: pre-emphasis + window of the 320 frame samples as 160 complex
 // (even, odd) pairs: lane j holds pair index 16*n1 + j, n1 = 0..9.
-template <bool MODE_B, bool SLOW, typename T>
-__device__ __forceinline__ void fe_stage0(const T* __restrict__ x, const Raw<T>& raw, int t, int n, int j,
+//   y[i] = x[i] - 0.97 x[i-1], y[0] = x[0]   (torchaudio preemphasis / mfcc.c:66-74)
+// On reflected rows (mode B edge frames) y(i0) = x[r] - 0.97 x[r-1] pairs
+// each sample with the NEXT one: own x1 for y0, the next lane's x0 for y1.
+template <bool MODE_B, typename T>
+__device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, int j, bool general,
                                           const FeTables& tb, cf (&a)[16]) {
-  const int base = MODE_B ? (256 * t - 160) : (256 * t);
   float prev_rot = 0.0f;
 #pragma unroll
   for (int n1 = 0; n1 < 10; ++n1) {
-    float y0, y1;
-    if constexpr (!SLOW) {
-      const float x0 = to_f(raw.x0[n1]), x1 = to_f(raw.x1[n1]);
-      // x[i0-1]: lane j-1's x1 of this row; lane 0 takes lane 15's x1 of the previous row.
-      const float rot = row_ror1(x1);
-      const float xm = j != 0 ? rot : (n1 == 0 ? to_f(raw.xb) : prev_rot);
-      prev_rot = rot;
-      y0 = __builtin_fmaf(-0.97f, xm, x0);
-      y1 = __builtin_fmaf(-0.97f, x0, x1);
-    } else {
+    const float x0 = to_f(raw.x0[n1]), x1 = to_f(raw.x1[n1]);
+    // x[i0-1]: lane j-1's x1 of this row; lane 0 takes lane 15's x1 of the previous row.
+    const float rot = row_ror1(x1);
+    const float xm = j != 0 ? rot : (n1 == 0 ? to_f(raw.xb) : prev_rot);
+    prev_rot = rot;
+    float y0 = __builtin_fmaf(-0.97f, xm, x0);
+    float y1 = __builtin_fmaf(-0.97f, x0, x1);
+    if (MODE_B && general) {
       const int i0 = base + 32 * n1 + 2 * j;
-      y0 = pre_general<MODE_B>(x, i0, n);
-      y1 = pre_general<MODE_B>(x, i0 + 1, n);
+      const float nx = row_rol1(x0);
+      const float xn = j != 15 ? nx : (n1 < 9 ? row_rol1(to_f(raw.x0[n1 + 1 < 10 ? n1 + 1 : 9])) : to_f(raw.xb));
+      if (i0 < 0 || i0 > n - 1) {
+        y0 = __builtin_fmaf(-0.97f, x1, x0);
+        y1 = __builtin_fmaf(-0.97f, xn, x1);
+      } else if (i0 == 0) {
+        y0 = x0;
+      }
     }
     const float2 w = *reinterpret_cast<const float2*>(tb.win + 32 * n1 + 2 * j);
     a[n1] = {y0 * w.x, y1 * w.y};

@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
     nfc = min(kNFramesB, nf - f0);
     fl = wave + 8 * r + slot_base;
     t = f0 + fl;
-    slow = MODE_B ? ((r == 0 && wave == 0) || (r == 1 && wave == 6)) : (chunk == 0 && r == 0 && wave == 0);
+    slow = MODE_B && ((r == 0 && wave == 0) || (r == 1 && wave == 6));   // holds frame 0 or 62
   };
   auto prefetch = [&](int64_t u, int r, Raw<T>& dst) {
     if (u < n_units) {
@@ -71,7 +71,8 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
       bool slow;
       const T* xp;
       frame_of(u, r, t, fl, nfc, slow, xp);
-      if (!slow) load_raw(xp, MODE_B ? 256 * t - 160 : 256 * t, j, fl < nfc, dst);
+      load_raw<MODE_B>(make_rsrc(xp, (uint32_t)win_len * sizeof(T)), MODE_B ? 256 * t - 160 : 256 * t, j, win_len,
+                       fl < nfc, slow, dst);
     }
   };
 
@@ -92,10 +93,7 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
       frame_of(u, r, t, fl, nfc_r, slow, xp);
       cf a[16];
       if (fl < nfc) {
-        if (slow)
-          fe_stage0<MODE_B, true>(xp, pf, t, win_len, j, tb, a);
-        else
-          fe_stage0<MODE_B, false>(xp, pf, t, win_len, j, tb, a);
+        fe_stage0<MODE_B>(pf, MODE_B ? 256 * t - 160 : 256 * t, win_len, j, slow, tb, a);
       }
       // pf is consumed: prefetch the next wave-round, (u,1) or (u+grid,0), into it.
       prefetch(r == 0 ? u : u + gridDim.x, r ^ 1, pf);

@@ -103,7 +103,8 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
     if (i < n_mine) {
       const int fl = wave + 8 * r + slot_base;
       const bool slow = (r == 0 && wave == 0) || (r == 1 && wave == 6);
-      if (!slow) load_raw(audio + clip_of(i) * clip_stride, 256 * fl - 160, j, fl < kNFramesB, dst);
+      load_raw<true>(make_rsrc(audio + clip_of(i) * clip_stride, kWinSamples * sizeof(T)), 256 * fl - 160, j,
+                     kWinSamples, fl < kNFramesB, slow, dst);
     }
   };
 
@@ -111,17 +112,13 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   prefetch(0, 0, pf);
   for (int64_t i = 0; i < n_mine; ++i) {
     const int64_t clip = clip_of(i);
-    const T* x = audio + clip * clip_stride;
 #pragma unroll 1
     for (int r = 0; r < 2; ++r) {
       const int fl = wave + 8 * r + slot_base;   // == frame index t (one chunk per clip)
       const bool slow = (r == 0 && wave == 0) || (r == 1 && wave == 6);
       cf a[16];
       if (fl < kNFramesB) {
-        if (slow)
-          fe_stage0<true, true>(x, pf, fl, kWinSamples, j, tb, a);
-        else
-          fe_stage0<true, false>(x, pf, fl, kWinSamples, j, tb, a);
+        fe_stage0<true>(pf, 256 * fl - 160, kWinSamples, j, slow, tb, a);
       }
       prefetch(r == 0 ? i : i + 1, r ^ 1, pf);
       if (fl < kNFramesB) fe_rest<true>(a, j, lane, P + fl * kPRow, tb, w512, 0);
