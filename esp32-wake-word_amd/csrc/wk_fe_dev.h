@@ -103,21 +103,24 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
   for (int n1 = 0; n1 < 10; ++n1) {
     const float x0 = to_f(raw.x0[n1]), x1 = to_f(raw.x1[n1]);
     // x[i0-1]: lane j-1's x1 of this row; lane 0 takes lane 15's x1 of the previous row.
-    const float rot = row_ror1(x1);
+    // DPP row rotates read other lanes: they must execute with the whole row
+    // active, so they are materialised (asm barrier) before any lane select.
+    float rot = row_ror1(x1);
+    asm volatile("" : "+v"(rot));
     const float xm = j != 0 ? rot : (n1 == 0 ? to_f(raw.xb) : prev_rot);
     prev_rot = rot;
     float y0 = __builtin_fmaf(-0.97f, xm, x0);
     float y1 = __builtin_fmaf(-0.97f, x0, x1);
     if (MODE_B && general) {
       const int i0 = base + 32 * n1 + 2 * j;
-      const float nx = row_rol1(x0);
-      const float xn = j != 15 ? nx : (n1 < 9 ? row_rol1(to_f(raw.x0[n1 + 1 < 10 ? n1 + 1 : 9])) : to_f(raw.xb));
-      if (i0 < 0 || i0 > n - 1) {
-        y0 = __builtin_fmaf(-0.97f, x1, x0);
-        y1 = __builtin_fmaf(-0.97f, xn, x1);
-      } else if (i0 == 0) {
-        y0 = x0;
-      }
+      float nx = row_rol1(x0);
+      float nx1 = row_rol1(to_f(raw.x0[n1 + 1 < 10 ? n1 + 1 : 9]));
+      asm volatile("" : "+v"(nx), "+v"(nx1));
+      const float xn = j != 15 ? nx : (n1 < 9 ? nx1 : to_f(raw.xb));
+      const bool reflected = i0 < 0 || i0 > n - 1;
+      const float r0 = __builtin_fmaf(-0.97f, x1, x0), r1 = __builtin_fmaf(-0.97f, xn, x1);
+      y0 = reflected ? r0 : (i0 == 0 ? x0 : y0);
+      y1 = reflected ? r1 : y1;
     }
     const float2 w = *reinterpret_cast<const float2*>(tb.win + 32 * n1 + 2 * j);
     a[n1] = {y0 * w.x, y1 * w.y};

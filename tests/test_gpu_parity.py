@@ -131,3 +131,20 @@ def test_error_paths(model):
         model.detect(np.zeros((2, 8000), np.float32))     # mode B needs 16000-sample windows
     out = model.detect(np.zeros((0, 16000), np.float32))
     assert out.shape == (0,)
+
+
+def test_frontend_raw_mfcc_every_frame(gpu):
+    """cmvn=0 exposes each frame separately: the reflected edge frames (0 and
+    62, torch.stft centre padding) must match like the interior ones."""
+    import wakeword
+    x = O.synth_clips(4321, 0, 6)
+    got = wakeword.mfcc(x, cmvn=False).cpu().numpy()
+    ref = O.mfcc_torchaudio(x)
+    per_frame = np.abs(got - ref).max(axis=(0, 1))
+    assert per_frame.shape == (63,)
+    assert per_frame.max() < 1e-3, np.argsort(-per_frame)[:4]
+    # int16 path through the same loader
+    xi = (x * 32768).clip(-32768, 32767).astype(np.int16)
+    gi = wakeword.mfcc(xi, cmvn=False).cpu().numpy()
+    ri = O.mfcc_torchaudio(xi.astype(np.float32) / 32768.0)
+    assert np.abs(gi - ri).max() < 1e-3
