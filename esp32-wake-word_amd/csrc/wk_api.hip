@@ -19,6 +19,7 @@ struct wk_handle {
   float* d_feats_ws;     // feature workspace for the unfused path
   int64_t ws_clips;
   int unfused;           // WAKEWORD_UNFUSED=1: front-end + CNN as two kernels (A/B testing)
+  int fused_exp;         // WAKEWORD_FUSED_EXP: role-isolation timing experiments (wrong logits)
 };
 
 namespace {
@@ -83,6 +84,8 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
   {
     const char* u = getenv("WAKEWORD_UNFUSED");
     h->unfused = u && u[0] == '1';
+    const char* fx = getenv("WAKEWORD_FUSED_EXP");
+    h->fused_exp = fx ? atoi(fx) : 0;
   }
   wk_status st = on_device(cfg->device, [&]() -> wk_status {
     hipDeviceProp_t prop;
@@ -185,7 +188,7 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
   return on_device(h->cfg.device, [&]() -> wk_status {
     if (!h->unfused) {
       hipError_t e = wk::launch_fused(dtype == WK_DTYPE_I16, d_audio, batch, clip_stride, h->d_packed, d_logits,
-                                      d_feats_or_null, h->n_cu, (hipStream_t)stream);
+                                      d_feats_or_null, h->n_cu, (hipStream_t)stream, h->fused_exp);
       return e == hipSuccess ? WK_OK : hip_fail(e, "fused launch");
     }
     const size_t esz = dtype == WK_DTYPE_I16 ? 2 : 4;

@@ -56,11 +56,11 @@ __device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g,
   for (int r = 0; r < 4; ++r) {
     float v = fmaxf(acc[r], 0.0f);
     v = fmaxf(v, swap_adjacent(v));
-    float s = w ? v : 0.0f;
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    s += __shfl_xor(s, 8, 64);
+    float s = w ? v : 0.0f;   // 16-lane row sum by DPP butterflies
+    s += dpp<0xB1>(s);
+    s += dpp<0x4E>(s);
+    s += dpp<0x141>(s);
+    s += dpp<0x140>(s);
     if (tt == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s / 7.0f;
   }
 }

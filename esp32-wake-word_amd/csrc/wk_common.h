@@ -11,18 +11,33 @@ constexpr int kPRow = 271;           // LDS pitch of one frame's power row (odd:
                                      // conflict-free; >=271 so the 16x17 transpose scratch fits)
 constexpr int kFeBlock = 512;        // 8 waves per front-end workgroup
 
-struct cf {
-  float re, im;
-};
+// Complex values live in VGPR pairs as float2 {re, im}: the front-end's
+// complex arithmetic then compiles to packed fp32 VALU (v_pk_add/mul/fma_f32,
+// two lanes' worth of fp32 per issue), swaps and sign flips folded into the
+// op_sel / neg modifiers.
+typedef float f2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ cf cadd(cf a, cf b) { return {a.re + b.re, a.im + b.im}; }
-__device__ __forceinline__ cf csub(cf a, cf b) { return {a.re - b.re, a.im - b.im}; }
-__device__ __forceinline__ cf cmul(cf a, cf b) {
-  return {__builtin_fmaf(a.re, b.re, -a.im * b.im), __builtin_fmaf(a.re, b.im, a.im * b.re)};
+__device__ __forceinline__ f2 swp(f2 a) { return __builtin_shufflevector(a, a, 1, 0); }
+__device__ __forceinline__ f2 bx(f2 a) { return __builtin_shufflevector(a, a, 0, 0); }
+__device__ __forceinline__ f2 by(f2 a) { return __builtin_shufflevector(a, a, 1, 1); }
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 sub_ib(f2 a, f2 b) { return fma2(swp(b), f2{1.0f, -1.0f}, a); }  // a - i b
+__device__ __forceinline__ f2 add_ib(f2 a, f2 b) { return fma2(swp(b), f2{-1.0f, 1.0f}, a); }  // a + i b
+
+// a * w, w = {c, s} a runtime twiddle: v_pk_mul + one v_pk_fma whose second
+// operand is w swizzled to {-s, s} by op_sel/neg_lo (the compiler would
+// build that pair with two extra VALU ops).
+__device__ __forceinline__ f2 cmul2(f2 a, f2 w) {
+  const f2 t = a * bx(w);
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
 }
+// a * w for a compile-time constant w.
+__device__ __forceinline__ f2 cmulc(f2 a, f2 w) { return fma2(swp(a), f2{-w.y, w.y}, a * f2{w.x, w.x}); }
 
-// cos / -sin of 2*pi*e/16 (forward-DFT twiddle W16^e = exp(-2*pi*i*e/16)).
-__device__ __forceinline__ cf w16(int e) {
+// W16^e = exp(-2*pi*i*e/16).
+__device__ __forceinline__ f2 w16(int e) {
   constexpr float c8 = 0.92387953251128674f, s8 = 0.38268343236508978f, h = 0.70710678118654752f;
   switch (e & 15) {
     case 0: return {1.f, 0.f};
@@ -44,30 +59,30 @@ __device__ __forceinline__ cf w16(int e) {
   }
 }
 
-// v * W16^e with the trivial quarter turns folded (e is a constant after unrolling).
-__device__ __forceinline__ cf twid16(cf v, int e) {
+// v * W16^e with the quarter turns folded (e is a constant after unrolling).
+__device__ __forceinline__ f2 twid16(f2 v, int e) {
   switch (e & 15) {
     case 0: return v;
-    case 4: return {v.im, -v.re};
-    case 8: return {-v.re, -v.im};
-    case 12: return {-v.im, v.re};
-    default: return cmul(v, w16(e));
+    case 4: return swp(v) * f2{1.0f, -1.0f};    // -i v
+    case 8: return -v;
+    case 12: return swp(v) * f2{-1.0f, 1.0f};   // i v
+    default: return cmulc(v, w16(e));
   }
 }
 
-// In-place 4-point forward DFT.
-__device__ __forceinline__ void dft4(cf& a0, cf& a1, cf& a2, cf& a3) {
-  const cf t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3), t3 = csub(a1, a3);
-  a0 = cadd(t0, t2);
-  a2 = csub(t0, t2);
-  a1 = {t1.re + t3.im, t1.im - t3.re};  // t1 - i t3
-  a3 = {t1.re - t3.im, t1.im + t3.re};  // t1 + i t3
+// In-place 4-point forward DFT (8 packed ops).
+__device__ __forceinline__ void dft4(f2& a0, f2& a1, f2& a2, f2& a3) {
+  const f2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = a1 - a3;
+  a0 = t0 + t2;
+  a2 = t0 - t2;
+  a1 = sub_ib(t1, t3);
+  a3 = add_ib(t1, t3);
 }
 
 // In-register 16-point forward DFT (radix 4x4).  Input a[n] natural order;
 // output A[k] lands in a[4*(k&3) + (k>>2)] (use dft16_out()).  Inputs known to
 // be zero at compile time fold away (built with -fno-signed-zeros).
-__device__ __forceinline__ void dft16(cf (&a)[16]) {
+__device__ __forceinline__ void dft16(f2 (&a)[16]) {
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb) dft4(a[nb], a[4 + nb], a[8 + nb], a[12 + nb]);
 #pragma unroll
@@ -98,10 +113,25 @@ __device__ __forceinline__ void wg_barrier_lds() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
+template <int CTRL> __device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the 64 lanes, result in every lane.  Within each 16-lane row the
+// butterflies are DPP (quad_perm xor1, xor2, row_half_mirror, row_mirror);
+// the four row sums are combined through SGPRs (v_readlane) -- no LDS
+// round trips (a __shfl_xor reduction is six dependent ds_bpermute).
+// Must be called with all 64 lanes active.
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return v;
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  v += dpp<0x140>(v);  // row_mirror
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
 }
 
 // Buffer-resource loads: base in SGPRs, per-lane byte offset in one VGPR, a
@@ -121,5 +151,29 @@ template <> __device__ __forceinline__ float sample<float>(const float* p, int64
 template <> __device__ __forceinline__ float sample<int16_t>(const int16_t* p, int64_t i) {
   return (float)p[i] * (1.0f / 32768.0f);
 }
+
+// Diagnostic builds only (-DWK_STAMPS, tools/debug): per-phase s_memtime
+// cycle sums.  Device helpers take an optional WkStamps* (WK_SP_PARAM) and
+// mark phase ends with WK_FE_HIT(k); product builds compile all of it away.
+#ifdef WK_STAMPS
+struct WkStamps {
+  unsigned long long st[16];
+  unsigned long long tl;
+  __device__ void init() {
+    for (int k = 0; k < 16; ++k) st[k] = 0;
+    tl = __builtin_amdgcn_s_memtime();
+  }
+  __device__ void hit(int k) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    st[k] += t - tl;
+    tl = t;
+  }
+};
+#define WK_SP_PARAM , WkStamps* stp = nullptr
+#define WK_FE_HIT(k) do { if (stp) stp->hit(k); } while (0)
+#else
+#define WK_SP_PARAM
+#define WK_FE_HIT(k) do {} while (0)
+#endif
 
 }  // namespace wk

@@ -8,7 +8,7 @@
 namespace wk {
 
 // W32^k2 = exp(-2*pi*i*k2/32), k2 = 0..8.
-__device__ __forceinline__ cf w32(int k2) {
+__device__ __forceinline__ f2 w32(int k2) {
   switch (k2) {
     case 0: return {1.0f, 0.0f};
     case 1: return {0.98078528040323043f, -0.19509032201612825f};
@@ -97,7 +97,7 @@ struct FeTables {
 // each sample with the NEXT one: own x1 for y0, the next lane's x0 for y1.
 template <bool MODE_B, typename T>
 __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, int j, bool general,
-                                          const FeTables& tb, cf (&a)[16]) {
+                                          const FeTables& tb, f2 (&a)[16] WK_SP_PARAM) {
   float prev_rot = 0.0f;
 #pragma unroll
   for (int n1 = 0; n1 < 10; ++n1) {
@@ -122,89 +122,101 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
       y0 = reflected ? r0 : (i0 == 0 ? x0 : y0);
       y1 = reflected ? r1 : y1;
     }
-    const float2 w = *reinterpret_cast<const float2*>(tb.win + 32 * n1 + 2 * j);
-    a[n1] = {y0 * w.x, y1 * w.y};
+    const f2 w = *reinterpret_cast<const f2*>(tb.win + 32 * n1 + 2 * j);
+    a[n1] = f2{y0, y1} * w;
   }
 #pragma unroll
-  for (int n1 = 10; n1 < 16; ++n1) a[n1] = {0.0f, 0.0f};
+  for (int n1 = 10; n1 < 16; ++n1) a[n1] = f2{0.0f, 0.0f};
 }
 
-// Stages 1..4 of one frame -> its power row (bins 0..256) in LDS.
+// Stages 1..4 of one frame -> its power row (bins 0..256) in LDS.  All
+// complex arithmetic is packed fp32 (see f2 in wk_common.h).
 template <bool MODE_B>
-__device__ __forceinline__ void fe_rest(cf (&a)[16], int j, int lane, float* __restrict__ row, const FeTables& tb,
-                                        cf w512, int esp_pack) {
+__device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __restrict__ row, const FeTables& tb,
+                                        f2 w512, int esp_pack WK_SP_PARAM) {
   dft16(a);  // A[k1] at a[dft16_out(k1)]
+  WK_FE_HIT(2);
 
   // twiddle W256^(j*k1) + 16x16 transpose through this frame's LDS row (pitch 17).
   // (twiddles are applied in groups of 4 so their LDS reads do not all
   // sit in VGPRs at once; re parts go straight to the transpose image.)
-  cf b[16];
+  f2 b[16];
   b[0] = a[0];
-  row[j] = b[0].re;
+  row[j] = b[0].x;
 #pragma unroll
   for (int k1 = 1; k1 < 16; ++k1) {
-    const float2 w = *reinterpret_cast<const float2*>(tb.tw + ((k1 - 1) * 16 + j) * 2);
-    b[k1] = cmul(a[dft16_out(k1)], cf{w.x, w.y});
-    row[17 * k1 + j] = b[k1].re;
+    const f2 w = *reinterpret_cast<const f2*>(tb.tw + ((k1 - 1) * 16 + j) * 2);
+    b[k1] = cmul2(a[dft16_out(k1)], w);
+    row[17 * k1 + j] = b[k1].x;
     if ((k1 & 3) == 3) __builtin_amdgcn_sched_barrier(0);
   }
-  cf c[16];
+  WK_FE_HIT(3);
+  f2 c[16];
   wave_lds_sync();
 #pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) c[n2].re = row[17 * j + n2];
+  for (int n2 = 0; n2 < 16; ++n2) c[n2].x = row[17 * j + n2];
   wave_lds_sync();
 #pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) row[17 * k1 + j] = b[k1].im;
+  for (int k1 = 0; k1 < 16; ++k1) row[17 * k1 + j] = b[k1].y;
   wave_lds_sync();
 #pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) c[n2].im = row[17 * j + n2];
+  for (int n2 = 0; n2 < 16; ++n2) c[n2].y = row[17 * j + n2];
   wave_lds_sync();
+  WK_FE_HIT(4);
 
   dft16(c);  // Z[j + 16*k2] at c[dft16_out(k2)]
+  WK_FE_HIT(5);
 
-  // Real-FFT split: U = 2 V[k] = S - i*b, U' = conj(2 V[256-k]) = S + i*b with
-  // S = Z[k] + conj Z[256-k], D = Z[k] - conj Z[256-k], b = W512^k D.
-  // Partner Z[256 - k]: lane (16-j)&15 of this group, register 15-k2 (ds_bpermute);
+  // Real-FFT split, k = j + 16*k2 (k2 = 0..8), with the partner Z[256 - k]:
+  //   S = Z[k] + conj Z[256-k],  D = Z[k] - conj Z[256-k],  bb = W512^k D,
+  //   U = 2 X[k] = S - i bb,  U' = conj(2 X[256-k]) = S + i bb
+  // (mode B folds the 1/4 of |X|^2 = |U|^2/4 into the filterbank weights).
+  // {|U|^2, |U'|^2} is one packed pair: {Ux, U'x}^2 + {Uy, U'y}^2.
+  // Partner: lane (16-j)&15 of this group, register 15-k2 (ds_bpermute);
   // lane 0 holds its own partner in register (16-k2)&15.
   const int src = ((lane & 48) | ((16 - j) & 15)) << 2;
+  f2 sc0 = {1.0f, 1.0f}, sc = {1.0f, 1.0f};
+  if constexpr (!MODE_B) {
+    // mfcc.c:267 power = |X|^2 / n_fft + 1e-12 = |U|^2 / 2048 + 1e-12; the
+    // esp-dsp dsps_cplx2reC_fc32 packing (mfcc.c:261) doubles bins 1..255
+    // (x4 in power) and zeroes bin 256 (parity unpinned).
+    const float e = esp_pack ? 4.0f / 2048.0f : 1.0f / 2048.0f;
+    sc = f2{e, e};
+    sc0 = esp_pack ? (j == 0 ? f2{1.0f / 2048.0f, 0.0f} : sc) : sc;  // j==0, k2==0: bins 0 and 256
+  }
 #pragma unroll
   for (int k2 = 0; k2 <= 8; ++k2) {
-    const cf zk = c[dft16_out(k2)];
-    cf zq_;
+    const f2 zk = c[dft16_out(k2)];
+    f2 zq;
     if (k2 < 8) {
-      const cf s = c[dft16_out(15 - k2)];
-      const cf own = c[dft16_out((16 - k2) & 15)];
-      const float pr = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.re)));
-      const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.im)));
-      zq_ = j == 0 ? own : cf{pr, pi};
+      const f2 s = c[dft16_out(15 - k2)];
+      const f2 own = c[dft16_out((16 - k2) & 15)];
+      const float pr = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.x)));
+      const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.y)));
+      zq = j == 0 ? own : f2{pr, pi};
     } else {
-      zq_ = c[dft16_out(8)];
+      zq = c[dft16_out(8)];
     }
-    const cf S = {zk.re + zq_.re, zk.im - zq_.im};
-    const cf D = {zk.re - zq_.re, zk.im + zq_.im};
-    const cf tw = cmul(w512, w32(k2));
-    const cf bb = cmul(tw, D);
-    const float ur = S.re + bb.im, ui = S.im - bb.re;
-    const float vr = S.re - bb.im, vi = S.im + bb.re;
-    float pk = __builtin_fmaf(ur, ur, ui * ui);
-    float pq = __builtin_fmaf(vr, vr, vi * vi);
+    const f2 S = fma2(zq, f2{1.0f, -1.0f}, zk);
+    const f2 D = fma2(zq, f2{-1.0f, 1.0f}, zk);
+    f2 Dw;
+    if (k2 == 0) Dw = D;
+    else if (k2 == 8) Dw = swp(D) * f2{1.0f, -1.0f};   // W32^8 = -i
+    else Dw = cmulc(D, w32(k2));
+    const f2 bb = cmul2(Dw, w512);
+    const f2 uvx = fma2(by(bb), f2{1.0f, -1.0f}, bx(S));
+    const f2 uvy = fma2(bx(bb), f2{-1.0f, 1.0f}, by(S));
+    f2 pw = fma2(uvx, uvx, uvy * uvy);
+    if constexpr (!MODE_B) pw = fma2(pw, k2 == 0 ? sc0 : sc, f2{1e-12f, 1e-12f});
     const int kb = j + 16 * k2;
-    if constexpr (!MODE_B) {
-      // mfcc.c:267 power = |X|^2 / n_fft + 1e-12 with |X|^2 = |U|^2 / 4; the
-      // esp-dsp dsps_cplx2reC_fc32 packing (mfcc.c:261) doubles bins 1..255
-      // and zeroes bin 256 (parity unpinned).
-      const float sk = esp_pack ? (kb == 0 ? 1.0f : 4.0f) : 1.0f;
-      const float sq = esp_pack ? (kb == 0 ? 0.0f : 4.0f) : 1.0f;  // kb==0 -> upper bin is 256
-      pk = __builtin_fmaf(pk, sk * (1.0f / 2048.0f), 1e-12f);
-      pq = __builtin_fmaf(pq, sq * (1.0f / 2048.0f), 1e-12f);
-    }
     if (k2 < 8) {
-      row[kb] = pk;
-      row[256 - kb] = pq;
+      row[kb] = pw.x;
+      row[256 - kb] = pw.y;
     } else if (j == 0) {
-      row[128] = pk;
+      row[128] = pw.x;
     }
   }
+  WK_FE_HIT(6);
 }
 
 template <bool MODE_B, int W>
@@ -233,7 +245,21 @@ __device__ __forceinline__ float cmvn_lane(float v, bool valid, int n) {
   const float d = valid ? v - mean : 0.0f;
   float sd = sqrtf(wave_sum(d * d) / (float)(n - 1));
   sd = sd == 0.0f ? 1.0f : sd;
-  return d / (sd + 1e-8f);
+  return d * (1.0f / (sd + 1e-8f));   // wave-uniform reciprocal
+}
+
+// Two independent coefficient rows at once (interleaved reductions).
+__device__ __forceinline__ void cmvn_lane2(float& v0, float& v1, bool valid, int n) {
+  const float m0 = wave_sum(valid ? v0 : 0.0f) / (float)n;
+  const float m1 = wave_sum(valid ? v1 : 0.0f) / (float)n;
+  const float d0 = valid ? v0 - m0 : 0.0f;
+  const float d1 = valid ? v1 - m1 : 0.0f;
+  float s0 = sqrtf(wave_sum(d0 * d0) / (float)(n - 1));
+  float s1 = sqrtf(wave_sum(d1 * d1) / (float)(n - 1));
+  s0 = s0 == 0.0f ? 1.0f : s0;
+  s1 = s1 == 0.0f ? 1.0f : s1;
+  v0 = d0 * (1.0f / (s0 + 1e-8f));
+  v1 = d1 * (1.0f / (s1 + 1e-8f));
 }
 
 // LDS carve (floats): twiddles | window | log-mel [40][64] | power rows [63][271].
@@ -257,10 +283,10 @@ __device__ __forceinline__ void fe_init_tables(float* smem, int tid, int nthread
   }
 }
 
-__device__ __forceinline__ cf fe_w512(int j) {
+__device__ __forceinline__ f2 fe_w512(int j) {
   float sn, cs;
   sincospif(-(float)j / 256.0f, &sn, &cs);
-  return {cs, sn};
+  return f2{cs, sn};
 }
 
 }  // namespace wk

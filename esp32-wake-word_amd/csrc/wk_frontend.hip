@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
 
   fe_init_tables<MODE_B>(smem, threadIdx.x, kFeBlock);
   const FeTables tb = {smem + kWinOff, smem + kTwOff};
-  const cf w512 = fe_w512(j);
+  const f2 w512 = fe_w512(j);
   // Frame slots: groups 0/1 (and 2/3) of a wave take frames 16 apart so their
   // pitch-17 transpose images fall in disjoint LDS banks.
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
       bool slow;
       const T* xp;
       frame_of(u, r, t, fl, nfc_r, slow, xp);
-      cf a[16];
+      f2 a[16];
       if (fl < nfc) {
         fe_stage0<MODE_B>(pf, MODE_B ? 256 * t - 160 : 256 * t, win_len, j, slow, tb, a);
       }

@@ -23,6 +23,20 @@ using namespace wk;
 
 namespace {
 
+#ifdef WK_STAMPS
+// Diagnostic build only (tools/debug): per-wave cycle sums per phase.
+__device__ unsigned long long g_wk_stamps[16][16];
+#define WK_STAMP_INIT WkStamps _stamps; _stamps.init();
+#define WK_STAMP(k) _stamps.hit(k)
+#define WK_STAMP_FLUSH(w) do { if (lane == 0) for (int _k = 0; _k < 16; ++_k) atomicAdd(&g_wk_stamps[w][_k], _stamps.st[_k]); } while (0)
+#define WK_SP_ARG , &_stamps
+#else
+#define WK_STAMP_INIT
+#define WK_STAMP(k) do {} while (0)
+#define WK_STAMP_FLUSH(w) do {} while (0)
+#define WK_SP_ARG
+#endif
+
 constexpr int NBF = 4;               // clips per CNN batch
 constexpr int kFusedBlock = 1024;    // 8 front-end + 8 CNN waves
 // CNN images (floats); ci pitches are 16 mod 32 (conflict-free B fragments).
@@ -86,72 +100,100 @@ __device__ __forceinline__ void signal_add(unsigned* ctrl, int idx, int lane) {
 // ---------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio, int64_t n_mine,
-                                        int64_t clip_stride, float* __restrict__ feats_out, int wave, int lane) {
+                                        int64_t clip_stride, float* __restrict__ feats_out, int wave, int lane,
+                                        int exp_flags) {
   float* P = smem + kPOff;
   float* L = smem + kLOff;
   float* F0 = smem + kF0Off;
   unsigned* ctrl = reinterpret_cast<unsigned*>(smem + kCtrlOff);
   const int g = lane >> 4, j = lane & 15;
   const FeTables tb = {smem + kWinOff, smem + kTwOff};
-  const cf w512 = fe_w512(j);
+  const f2 w512 = fe_w512(j);
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);
   const int64_t G = gridDim.x;
   unsigned gen = 0;
 
+  // Static frame assignment: wave w, round r, lane group g takes frame
+  // w + 8r + 16(g&1) + 32(g>>1) (groups 0/1 16 frames apart: disjoint LDS
+  // banks).  A dynamic hand-out through an LDS counter was measured slower:
+  // the atomic's return latency lands on the prefetch path.
   auto clip_of = [&](int64_t i) { return (int64_t)blockIdx.x + G * i; };
   auto prefetch = [&](int64_t i, int r, Raw<T>& dst) {
     if (i < n_mine) {
       const int fl = wave + 8 * r + slot_base;
-      const bool slow = (r == 0 && wave == 0) || (r == 1 && wave == 6);
+      const bool general = (r == 0 && wave == 0) || (r == 1 && wave == 6);   // frame 0 / frame 62
       load_raw<true>(make_rsrc(audio + clip_of(i) * clip_stride, kWinSamples * sizeof(T)), 256 * fl - 160, j,
-                     kWinSamples, fl < kNFramesB, slow, dst);
+                     kWinSamples, fl < kNFramesB, general, dst);
     }
   };
 
   Raw<T> pf;
   prefetch(0, 0, pf);
+  WK_STAMP_INIT
   for (int64_t i = 0; i < n_mine; ++i) {
     const int64_t clip = clip_of(i);
 #pragma unroll 1
     for (int r = 0; r < 2; ++r) {
       const int fl = wave + 8 * r + slot_base;   // == frame index t (one chunk per clip)
-      const bool slow = (r == 0 && wave == 0) || (r == 1 && wave == 6);
-      cf a[16];
-      if (fl < kNFramesB) {
-        fe_stage0<true>(pf, 256 * fl - 160, kWinSamples, j, slow, tb, a);
-      }
+      const bool general = (r == 0 && wave == 0) || (r == 1 && wave == 6);
+      f2 a[16];
+      if (fl < kNFramesB) fe_stage0<true>(pf, 256 * fl - 160, kWinSamples, j, general, tb, a);
+      WK_STAMP(0);
       prefetch(r == 0 ? i : i + 1, r ^ 1, pf);
-      if (fl < kNFramesB) fe_rest<true>(a, j, lane, P + fl * kPRow, tb, w512, 0);
+      WK_STAMP(1);
+      if (fl < kNFramesB) fe_rest<true>(a, j, lane, P + fl * kPRow, tb, w512, 0 WK_SP_ARG);
     }
     role_sync(ctrl, kCtrlFeBar, gen, lane);
-
+    WK_STAMP(7);
     mel_dispatch<true>(wave, P + min(lane, kNFramesB - 1) * kPRow, L + lane);
+    WK_STAMP(8);
     role_sync(ctrl, kCtrlFeBar, gen, lane);
+    WK_STAMP(9);
 
     const int64_t b = i / NBF;
     const int s = (int)(i - b * NBF);
-    if (s == 0 && b > 0) spin_until(ctrl, kCtrlAct0Free, (unsigned)b);   // CNN done reading batch b-1
-    const float* lrow = L + lane;
-    const bool valid = lane < kNFramesB;
-    const int c0 = wave < 5 ? 2 * wave : wave + 5;
-    const int nc = wave < 5 ? 2 : 1;
-    for (int ci = 0; ci < nc; ++ci) {
-      const int cc = c0 + ci;
+    if (s == 0 && b > 0 && !(exp_flags & 1)) spin_until(ctrl, kCtrlAct0Free, (unsigned)b);   // CNN done with b-1
+    WK_STAMP(10);
+    // Recompute lane-dependent addresses here: hoisted out of the clip loop
+    // they are spilled to scratch, and a scratch reload waits on vmcnt(0) --
+    // i.e. on the audio prefetch in flight.
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const float* lrow = L + ln;
+    const bool valid = ln < kNFramesB;
+    // 13 coefficients over 8 waves: waves 0-4 take two (reductions
+    // interleaved), waves 5-7 one.
+    if (wave < 5) {
+      const int c0 = 2 * wave;
+      float y0 = dct_coef<true>(c0, lrow), y1 = dct_coef<true>(c0 + 1, lrow);
+      cmvn_lane2(y0, y1, valid, kNFramesB);
+      if (valid) {
+        F0[c0 * F0_CI + s * F0_CLIP + 1 + ln] = y0;
+        F0[(c0 + 1) * F0_CI + s * F0_CLIP + 1 + ln] = y1;
+        if (feats_out) {
+          feats_out[clip * (13 * kNFramesB) + c0 * kNFramesB + ln] = y0;
+          feats_out[clip * (13 * kNFramesB) + (c0 + 1) * kNFramesB + ln] = y1;
+        }
+      }
+    } else {
+      const int cc = wave + 5;
       const float y = cmvn_lane(dct_coef<true>(cc, lrow), valid, kNFramesB);
       if (valid) {
-        F0[cc * F0_CI + s * F0_CLIP + 1 + lane] = y;
-        if (feats_out) feats_out[clip * (13 * kNFramesB) + cc * kNFramesB + lane] = y;
+        F0[cc * F0_CI + s * F0_CLIP + 1 + ln] = y;
+        if (feats_out) feats_out[clip * (13 * kNFramesB) + cc * kNFramesB + ln] = y;
       }
     }
+    WK_STAMP(11);
     if (s == NBF - 1 || i == n_mine - 1) signal_add(ctrl, kCtrlFeatReady, lane);
   }
+  WK_STAMP_FLUSH(wave);
 }
 
 // ---------------------------------------------------------------------------
 // CNN role (waves 8-15): batches of NBF clips from the conv1 image.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ pk, int64_t n_mine,
-                                         float* __restrict__ logits, int cw, int lane) {
+                                         float* __restrict__ logits, int cw, int lane, int exp_flags) {
   float* F0 = smem + kF0Off;
   float* F1 = smem + kF1Off;
   float* F2 = smem + kF2Off;
@@ -173,13 +215,15 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
   }
   const int64_t n_batches = (n_mine + NBF - 1) / NBF;
+  WK_STAMP_INIT
   for (int64_t b = 0; b < n_batches; ++b) {
     float w1[12];
     {
 #pragma unroll
       for (int s = 0; s < 12; ++s) w1[s] = buf_load(rs, lv, 4 * (kPkW1 + ((cw & 1) * 12 + s) * 64));
     }
-    spin_until(ctrl, kCtrlFeatReady, 8u * (unsigned)(b + 1));
+    if (!(exp_flags & 2)) spin_until(ctrl, kCtrlFeatReady, 8u * (unsigned)(b + 1));
+    WK_STAMP(0);
 
     // conv1: co tile (cw&1), clip (cw>>1), 4 t-tiles.
     {
@@ -194,7 +238,9 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         epi_pool<F1_CI, F1_CLIP, 31>(acc_b, F1, co0, cl, tb, lane);
       }
     }
+    WK_STAMP(1);
     role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    WK_STAMP(2);
     if (cw == 0) signal_add(ctrl, kCtrlAct0Free, lane);   // front-end may overwrite the conv1 image
 
     // conv2: co tile (cw&3), clips 2*(cw>>2) + {0,1}, 2 t-tiles each.
@@ -213,7 +259,9 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         epi_pool<F2_CI, F2_CLIP, 15>(acc_b, F2, co0, cl, 16, lane);
       }
     }
+    WK_STAMP(3);
     role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    WK_STAMP(4);
 
     // conv3: co tile cw, the 4 clips; GAP -> G[128][4].
     {
@@ -233,7 +281,9 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 #pragma unroll
       for (int s = 0; s < 16; ++s) wf1[s] = buf_load(rs, lv, 4 * (kPkF1 + ((cw & 3) * 32 + 16 * (cw >> 2) + s) * 64));
     }
+    WK_STAMP(5);
     role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    WK_STAMP(6);
 
     // classifier.0 (128 -> 64): o tile (cw&3), k half (cw>>2); columns >= NBF are don't-care.
     {
@@ -247,6 +297,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
       }
     }
     role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    WK_STAMP(7);
 
     // ReLU -> classifier.2 (64 -> 1): lane = (o group q = lane>>2, clip = lane&3).
     if (cw == 0) {
@@ -265,14 +316,16 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
       const int64_t i = b * NBF + cl;
       if (q == 0 && i < n_mine) logits[(int64_t)blockIdx.x + G * i] = acc;
     }
+    WK_STAMP(8);
   }
+  WK_STAMP_FLUSH(8 + cw);
 }
 
 template <typename T>
 __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __restrict__ audio, int64_t batch,
                                                                  int64_t clip_stride, const float* __restrict__ wts,
                                                                  float* __restrict__ logits,
-                                                                 float* __restrict__ feats_out) {
+                                                                 float* __restrict__ feats_out, int exp_flags) {
   __shared__ __attribute__((aligned(16))) float smem[kFusedLds];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -283,29 +336,40 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
   const int64_t n_mine = batch > (int64_t)blockIdx.x ? (batch - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   if (wave < 8) {
 #ifndef WK_EXPERIMENT_NO_FE
-    fe_role<T>(smem, audio, n_mine, clip_stride, feats_out, wave, lane);
+    if (!(exp_flags & 2)) fe_role<T>(smem, audio, n_mine, clip_stride, feats_out, wave, lane, exp_flags);
 #endif
   } else {
 #ifndef WK_EXPERIMENT_NO_CNN
-    cnn_role(smem, wts, n_mine, logits, wave - 8, lane);
+    if (!(exp_flags & 1)) cnn_role(smem, wts, n_mine, logits, wave - 8, lane, exp_flags);
 #endif
   }
 }
 
 }  // namespace
 
+#ifdef WK_STAMPS
+extern "C" int wk_debug_stamps(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wk_stamps), sizeof(g_wk_stamps)) != hipSuccess) return 1;
+  if (reset) {
+    static unsigned long long zero[16][16];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_wk_stamps), zero, sizeof(zero)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
+
 namespace wk {
 
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
-                        float* logits, float* feats_or_null, int grid_cap, hipStream_t stream) {
+                        float* logits, float* feats_or_null, int grid_cap, hipStream_t stream, int exp_flags) {
   if (batch == 0) return hipSuccess;
   const int grid = (int)(batch < grid_cap ? batch : grid_cap);
   if (i16)
     hipLaunchKernelGGL(wk_fused_kernel<int16_t>, dim3(grid), dim3(kFusedBlock), 0, stream, (const int16_t*)audio,
-                       batch, clip_stride, w, logits, feats_or_null);
+                       batch, clip_stride, w, logits, feats_or_null, exp_flags);
   else
     hipLaunchKernelGGL(wk_fused_kernel<float>, dim3(grid), dim3(kFusedBlock), 0, stream, (const float*)audio, batch,
-                       clip_stride, w, logits, feats_or_null);
+                       clip_stride, w, logits, feats_or_null, exp_flags);
   return hipGetLastError();
 }
 

@@ -18,7 +18,8 @@ hipError_t launch_cnn(const float* feats, int64_t batch, const float* w, float* 
 
 // Fused front-end + CNN (wk_fused.hip), mode B only.
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
-                        float* logits, float* feats_or_null, int grid_cap, hipStream_t stream);
+                        float* logits, float* feats_or_null, int grid_cap, hipStream_t stream,
+                        int exp_flags = 0);   // exp_flags (timing experiments only): 1 = FE role only, 2 = CNN only
 
 // Misc (wk_misc.hip).
 hipError_t launch_synth(uint32_t seed, int64_t first, int64_t count, int n, float* out, hipStream_t stream);

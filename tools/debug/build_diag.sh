@@ -1,0 +1,11 @@
+#!/bin/bash
+# Diagnostic library with in-kernel s_memtime phase stamps (never the product).
+set -e
+R=$(cd "$(dirname "$0")/../.." && pwd)
+cd "$R/esp32-wake-word_amd"
+HIPCC=/opt/rocm/bin/hipcc
+FL="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -fno-signed-zeros -ffp-contract=fast -fno-slp-vectorize -I $R/include -I csrc -DWK_STAMPS"
+mkdir -p build/diag
+for f in wk_frontend wk_cnn wk_fused wk_misc wk_api; do $HIPCC $FL -c csrc/$f.hip -o build/diag/$f.o & done; wait
+$HIPCC --offload-arch=gfx950 -shared -fPIC build/diag/*.o -o build/diag/libwakeword_diag.so
+echo "$R/esp32-wake-word_amd/build/diag/libwakeword_diag.so"
