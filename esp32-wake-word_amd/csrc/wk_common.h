@@ -143,6 +143,12 @@ __device__ __forceinline__ float buf_load(__amdgpu_buffer_rsrc_t r, int voff, in
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
 
+// Natural log for the log-mel stage: v_log_f32 (log2, ~1 ulp; arguments are
+// >= 1e-12, never denormal) times ln 2, instead of the ~20-instruction libm
+// expansion.  Differs from torch.log by ~1e-7 relative (parity tolerance
+// of the features is 5e-4).
+__device__ __forceinline__ float wk_logf(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
+
 __device__ __forceinline__ float to_f(float v) { return v; }
 __device__ __forceinline__ float to_f(int16_t v) { return (float)v * (1.0f / 32768.0f); }
 

@@ -5,6 +5,10 @@
 #include "wk_common.h"
 #include "wk_tables.h"
 
+#ifndef WK_TW_GROUP
+#define WK_TW_GROUP 0   // >0: fence the twiddle LDS reads into groups of this many (0 = compiler schedules; measured equal)
+#endif
+
 namespace wk {
 
 // W32^k2 = exp(-2*pi*i*k2/32), k2 = 0..8.
@@ -148,7 +152,7 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
     const f2 w = *reinterpret_cast<const f2*>(tb.tw + ((k1 - 1) * 16 + j) * 2);
     b[k1] = cmul2(a[dft16_out(k1)], w);
     row[17 * k1 + j] = b[k1].x;
-    if ((k1 & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    if (WK_TW_GROUP > 0 && (k1 % (WK_TW_GROUP > 0 ? WK_TW_GROUP : 1)) == WK_TW_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
   }
   WK_FE_HIT(3);
   f2 c[16];

@@ -3,18 +3,20 @@
 //   audio (HBM) -> MFCC front-end (VALU/LDS) -> features (LDS) -> xiaoa CNN
 //   (fp32 MFMA) -> logit (HBM)
 //
-// One 16-wave workgroup per CU.  Waves 0-7 run the front-end of wk_frontend.hip
-// clip after clip (FFT / lane-per-frame mel / DCT + CMVN, see wk_fe_dev.h) and
-// write each clip's CMVN'd [13][63] features straight into the CNN's conv1
-// input image in LDS.  Waves 8-15 run the CNN of wk_cnn.hip on batches of
-// NBF = 4 clips from that image.  The two roles share no s_barrier: each role
-// synchronises its own 8 waves through an LDS counter barrier, and the
-// hand-off is two LDS counters (features ready / conv1 input free).  The
-// front-end is VALU + LDS bound and the CNN is MFMA bound; on CDNA4 the
-// matrix and vector pipes issue concurrently from different waves, so the
-// two roles overlap on every SIMD (2 front-end + 2 CNN waves per SIMD), and
-// features never touch HBM: per clip the kernel reads its 64,000 audio bytes
-// and writes one 4-byte logit.
+// One 16-wave workgroup per CU.  Waves 0-7 (front-end role) run the FFT and
+// the lane-per-frame mel filterbank of wk_fe_dev.h clip after clip and write
+// each clip's log-mel image [40][63] into one of two LDS buffers.  Waves 8-15
+// (CNN role) take the DCT-II + CMVN from that buffer into the conv1 input
+// image, then run the CNN of wk_cnn.hip on batches of NBF = 4 clips.  The
+// roles share no s_barrier: each synchronises its own 8 waves through an LDS
+// counter barrier, and the hand-off is two LDS counters (log-mel ready /
+// log-mel buffer free).  Moving the DCT + CMVN to the CNN waves (which wait
+// on the front-end about half the time) shortened the front-end's per-clip
+// critical path by ~15 %.  The front-end is VALU + LDS bound and the CNN is
+// MFMA bound; on CDNA4 the matrix and vector pipes issue concurrently from
+// different waves, so the roles overlap on every SIMD (2 front-end + 2 CNN
+// waves per SIMD), and features never touch HBM: per clip the kernel reads
+// its 64,000 audio bytes and writes one 4-byte logit.
 #include "wk_cnn_dev.h"
 #include "wk_fe_dev.h"
 #include "wk_kernels.h"
@@ -49,11 +51,12 @@ constexpr int kF1Off = kF0Off + 16 * F0_CI;
 constexpr int kF2Off = kF1Off + 32 * F1_CI;
 constexpr int kGOff = kF2Off + 64 * F2_CI;          // pooled features [128][4]
 constexpr int kFcpOff = kGOff + 128 * NBF;          // classifier.0 partials [2][64][4]
-constexpr int kCtrlOff = kFcpOff + 2 * 64 * NBF;    // control words
+constexpr int kL1Off = kFcpOff + 2 * 64 * NBF;      // second log-mel buffer [40][64] (first: kLOff)
+constexpr int kCtrlOff = kL1Off + kLSize;           // control words
 constexpr int kFusedLds = kCtrlOff + 16;
 static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 
-enum { kCtrlFeBar = 0, kCtrlCnnBar = 1, kCtrlFeatReady = 2, kCtrlAct0Free = 3, kCtrlAbort = 15 };
+enum { kCtrlFeBar = 0, kCtrlCnnBar = 1, kCtrlLReady = 2, kCtrlLFree = 3, kCtrlAbort = 15 };
 // Every spin is bounded (~4M sleeps, well under a second): a protocol bug
 // yields wrong logits and a drained grid, never a hung GPU.
 constexpr unsigned kSpinLimit = 1u << 22;
@@ -104,14 +107,14 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
                                         int exp_flags) {
   float* P = smem + kPOff;
   float* L = smem + kLOff;
-  float* F0 = smem + kF0Off;
+  float* L1 = smem + kL1Off;
   unsigned* ctrl = reinterpret_cast<unsigned*>(smem + kCtrlOff);
   const int g = lane >> 4, j = lane & 15;
   const FeTables tb = {smem + kWinOff, smem + kTwOff};
   const f2 w512 = fe_w512(j);
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);
   const int64_t G = gridDim.x;
-  unsigned gen = 0;
+  unsigned gen = 0, p_wait = 0;
 
   // Static frame assignment: wave w, round r, lane group g takes frame
   // w + 8r + 16(g&1) + 32(g>>1) (groups 0/1 16 frames apart: disjoint LDS
@@ -131,60 +134,39 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   prefetch(0, 0, pf);
   WK_STAMP_INIT
   for (int64_t i = 0; i < n_mine; ++i) {
-    const int64_t clip = clip_of(i);
 #pragma unroll 1
     for (int r = 0; r < 2; ++r) {
       const int fl = wave + 8 * r + slot_base;   // == frame index t (one chunk per clip)
       const bool general = (r == 0 && wave == 0) || (r == 1 && wave == 6);
+      if (exp_flags & 4) {   // alternate issue priority between the two front-end waves of a SIMD
+        if ((wave >= 4) == (r == 1)) __builtin_amdgcn_s_setprio(2); else __builtin_amdgcn_s_setprio(1);
+      } else if (exp_flags & 8) {
+        if ((wave >= 4) == (r == 1)) __builtin_amdgcn_s_setprio(1); else __builtin_amdgcn_s_setprio(0);
+      }
       f2 a[16];
       if (fl < kNFramesB) fe_stage0<true>(pf, 256 * fl - 160, kWinSamples, j, general, tb, a);
       WK_STAMP(0);
       prefetch(r == 0 ? i : i + 1, r ^ 1, pf);
       WK_STAMP(1);
+      if (r == 0) {
+        spin_until(ctrl, kCtrlFeBar, p_wait);   // every wave done reading clip i-1's power rows
+        WK_STAMP(9);
+      }
       if (fl < kNFramesB) fe_rest<true>(a, j, lane, P + fl * kPRow, tb, w512, 0 WK_SP_ARG);
     }
-    role_sync(ctrl, kCtrlFeBar, gen, lane);
+    if (exp_flags & 4) __builtin_amdgcn_s_setprio(1); else if (exp_flags & 8) __builtin_amdgcn_s_setprio(0);
+    role_sync(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
     WK_STAMP(7);
-    mel_dispatch<true>(wave, P + min(lane, kNFramesB - 1) * kPRow, L + lane);
-    WK_STAMP(8);
-    role_sync(ctrl, kCtrlFeBar, gen, lane);
-    WK_STAMP(9);
-
-    const int64_t b = i / NBF;
-    const int s = (int)(i - b * NBF);
-    if (s == 0 && b > 0 && !(exp_flags & 1)) spin_until(ctrl, kCtrlAct0Free, (unsigned)b);   // CNN done with b-1
+    if (i >= 2 && !(exp_flags & 1)) spin_until(ctrl, kCtrlLFree, 8u * (unsigned)(i - 1));   // clip i-2's DCT done
     WK_STAMP(10);
-    // Recompute lane-dependent addresses here: hoisted out of the clip loop
-    // they are spilled to scratch, and a scratch reload waits on vmcnt(0) --
-    // i.e. on the audio prefetch in flight.
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const float* lrow = L + ln;
-    const bool valid = ln < kNFramesB;
-    // 13 coefficients over 8 waves: waves 0-4 take two (reductions
-    // interleaved), waves 5-7 one.
-    if (wave < 5) {
-      const int c0 = 2 * wave;
-      float y0 = dct_coef<true>(c0, lrow), y1 = dct_coef<true>(c0 + 1, lrow);
-      cmvn_lane2(y0, y1, valid, kNFramesB);
-      if (valid) {
-        F0[c0 * F0_CI + s * F0_CLIP + 1 + ln] = y0;
-        F0[(c0 + 1) * F0_CI + s * F0_CLIP + 1 + ln] = y1;
-        if (feats_out) {
-          feats_out[clip * (13 * kNFramesB) + c0 * kNFramesB + ln] = y0;
-          feats_out[clip * (13 * kNFramesB) + (c0 + 1) * kNFramesB + ln] = y1;
-        }
-      }
-    } else {
-      const int cc = wave + 5;
-      const float y = cmvn_lane(dct_coef<true>(cc, lrow), valid, kNFramesB);
-      if (valid) {
-        F0[cc * F0_CI + s * F0_CLIP + 1 + ln] = y;
-        if (feats_out) feats_out[clip * (13 * kNFramesB) + cc * kNFramesB + ln] = y;
-      }
-    }
-    WK_STAMP(11);
-    if (s == NBF - 1 || i == n_mine - 1) signal_add(ctrl, kCtrlFeatReady, lane);
+    mel_dispatch<true>(wave, P + min(lane, kNFramesB - 1) * kPRow, (i & 1 ? L1 : L) + lane);
+    WK_STAMP(8);
+    signal_add(ctrl, kCtrlLReady, lane);
+    // Split barrier: arrive now, wait before this wave next writes a power
+    // row (round 0 of clip i+1), after its stage 0 and prefetch.
+    gen += 8;
+    signal_add(ctrl, kCtrlFeBar, lane);
+    p_wait = gen;
   }
   WK_STAMP_FLUSH(wave);
 }
@@ -193,7 +175,10 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
 // CNN role (waves 8-15): batches of NBF clips from the conv1 image.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ pk, int64_t n_mine,
-                                         float* __restrict__ logits, int cw, int lane, int exp_flags) {
+                                         float* __restrict__ logits, float* __restrict__ feats_out, int cw, int lane,
+                                         int exp_flags) {
+  const float* L = smem + kLOff;
+  const float* L1 = smem + kL1Off;
   float* F0 = smem + kF0Off;
   float* F1 = smem + kF1Off;
   float* F2 = smem + kF2Off;
@@ -222,8 +207,47 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 #pragma unroll
       for (int s = 0; s < 12; ++s) w1[s] = buf_load(rs, lv, 4 * (kPkW1 + ((cw & 1) * 12 + s) * 64));
     }
-    if (!(exp_flags & 2)) spin_until(ctrl, kCtrlFeatReady, 8u * (unsigned)(b + 1));
+    // DCT-II + CMVN of the batch's clips (extract_mfcc.py:70-80) from the
+    // double-buffered log-mel image into the conv1 input image.  Coefficient
+    // sets (k < 5: coefficients 2k, 2k+1; k >= 5: k+5) rotate over the waves
+    // per clip, so over a batch every wave does 6 or 7 coefficients.
+    {
+      const int nb = (int)(n_mine - b * NBF < NBF ? n_mine - b * NBF : NBF);
+      int ln = lane;
+      asm volatile("" : "+v"(ln));   // keep lane addressing out of the loop-invariant (spilled) set
+      const bool valid = ln < kNFramesB;
+      for (int s = 0; s < nb; ++s) {
+        const int64_t i = b * NBF + s;
+        if (!(exp_flags & 2)) spin_until(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
+        const float* lrow = (i & 1 ? L1 : L) + ln;
+        const int k = (cw + 3 * s) & 7;
+        float* f0 = F0 + s * F0_CLIP + 1 + ln;
+        float* fo = feats_out ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) + ln : nullptr;
+        if (k < 5) {
+          const int c0 = 2 * k;
+          float y0 = dct_coef<true>(c0, lrow), y1 = dct_coef<true>(c0 + 1, lrow);
+          cmvn_lane2(y0, y1, valid, kNFramesB);
+          if (valid) {
+            f0[c0 * F0_CI] = y0;
+            f0[(c0 + 1) * F0_CI] = y1;
+            if (fo) {
+              fo[c0 * kNFramesB] = y0;
+              fo[(c0 + 1) * kNFramesB] = y1;
+            }
+          }
+        } else {
+          const int c0 = k + 5;
+          const float y = cmvn_lane(dct_coef<true>(c0, lrow), valid, kNFramesB);
+          if (valid) {
+            f0[c0 * F0_CI] = y;
+            if (fo) fo[c0 * kNFramesB] = y;
+          }
+        }
+        signal_add(ctrl, kCtrlLFree, lane);   // this wave's reads of the log-mel buffer are done
+      }
+    }
     WK_STAMP(0);
+    role_sync(ctrl, kCtrlCnnBar, gen, lane);   // conv1 image complete
 
     // conv1: co tile (cw&1), clip (cw>>1), 4 t-tiles.
     {
@@ -241,7 +265,6 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     WK_STAMP(1);
     role_sync(ctrl, kCtrlCnnBar, gen, lane);
     WK_STAMP(2);
-    if (cw == 0) signal_add(ctrl, kCtrlAct0Free, lane);   // front-end may overwrite the conv1 image
 
     // conv2: co tile (cw&3), clips 2*(cw>>2) + {0,1}, 2 t-tiles each.
     {
@@ -287,6 +310,9 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 
     // classifier.0 (128 -> 64): o tile (cw&3), k half (cw>>2); columns >= NBF are don't-care.
     {
+      int ln = lane;
+      asm volatile("" : "+v"(ln));   // addresses recomputed here rather than kept live (and spilled)
+      const int li = ln & 15, lk = ln >> 4;
       f32x4 acc = {0, 0, 0, 0};
       const int kh = cw >> 2;
 #pragma unroll
@@ -301,7 +327,9 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 
     // ReLU -> classifier.2 (64 -> 1): lane = (o group q = lane>>2, clip = lane&3).
     if (cw == 0) {
-      const int cl = lane & (NBF - 1), q = lane >> 2;
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int cl = ln & (NBF - 1), q = ln >> 2;
       float acc = 0.0f;
 #pragma unroll
       for (int i2 = 0; i2 < 4; ++i2) {
@@ -340,7 +368,7 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
 #endif
   } else {
 #ifndef WK_EXPERIMENT_NO_CNN
-    if (!(exp_flags & 1)) cnn_role(smem, wts, n_mine, logits, wave - 8, lane, exp_flags);
+    if (!(exp_flags & 1)) cnn_role(smem, wts, n_mine, logits, feats_out, wave - 8, lane, exp_flags);
 #endif
   }
 }

@@ -166,9 +166,9 @@ def emit_mel(fb: np.ndarray, name: str, mode: str, scale: float):
                                  for m, wt in terms) + " }")
         for m in range(a, b):
             if mode == "B":
-                lines.append(f"  l[{m} * WK_LSTRIDE] = logf(a{m} + 1e-6f);")
+                lines.append(f"  l[{m} * WK_LSTRIDE] = wk::wk_logf(a{m} + 1e-6f);")
             else:
-                lines.append(f"  l[{m} * WK_LSTRIDE] = logf(__builtin_fmaxf(a{m}, 1e-12f));")
+                lines.append(f"  l[{m} * WK_LSTRIDE] = wk::wk_logf(__builtin_fmaxf(a{m}, 1e-12f));")
         lines.append("}")
     lines.append(f"template <int W> __device__ __forceinline__ void {name}_wave(const float* p, float* l);")
     for w in range(N_WAVES):

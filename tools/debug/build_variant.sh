@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build a variant of the library with extra compile flags (experiments only):
+#   bash tools/debug/build_variant.sh <name> [-DFOO=1 ...]  -> build/var_<name>/libwakeword.so
+set -e
+R=$(cd "$(dirname "$0")/../.." && pwd)
+NAME=$1; shift
+cd "$R/esp32-wake-word_amd"
+HIPCC=/opt/rocm/bin/hipcc
+FL="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -fno-signed-zeros -ffp-contract=fast -fno-slp-vectorize -I $R/include -I csrc $*"
+D=build/var_$NAME
+mkdir -p $D
+for f in wk_frontend wk_cnn wk_fused wk_misc wk_api; do $HIPCC $FL -c csrc/$f.hip -o $D/$f.o & done; wait
+$HIPCC --offload-arch=gfx950 -shared -fPIC $D/*.o -o $D/libwakeword.so
+echo "$R/esp32-wake-word_amd/$D/libwakeword.so"
