@@ -148,7 +148,7 @@ def main():
         achieved = FLOP_PER_WINDOW * B / (launch_ms * 1e-3) / 1e12
         traffic_bpw, traffic_src = load_traffic()
         out = {
-            "metric": "audio windows/sec (1s@16kHz, 40-MFCC) through xiaoa CNN",
+            "metric": "audio windows/sec (1s@16kHz, 40-MFCC) through xiaoa CNN at 1/2/4/8 MI355X",
             "value": round(value, 1),
             "unit": "windows/s",
             "n_gpus": world,
