@@ -227,3 +227,73 @@ def synth_clips(seed: int, first: int, count: int, n: int = WIN_SAMPLES) -> np.n
     phase = ((s * np.uint64(440)) % np.uint64(16000)).astype(np.float32) * np.float32(1.0 / 16000.0)
     sine = (np.float32(0.1) * np.sin(np.float32(2.0 * np.pi) * phase)).astype(np.float32)
     return np.where(odd, x + sine, x).astype(np.float32)
+
+
+# --------------------------------------------------------------------------
+# Front-end mode A: main/esp_mfcc/mfcc.c:431-527 (numpy restatement; the C
+# restatement is oracle/esp_mfcc_oracle.c -- the two cross-check each other,
+# no reference fixture pins mode-A values: "parity unpinned").
+# --------------------------------------------------------------------------
+def fbank_mode_a(sr: int = SAMPLE_RATE, n_filters: int = N_MELS, n_fft: int = N_FFT) -> np.ndarray:
+    """(n_fft/2+1, n_filters) integer-bin triangles (mfcc.c:133-234), float32
+    arithmetic as in the C code (hz_to_mel 1127 ln(1+f/700), f=0 -> 1; the
+    inverse uses 700 (10^(m/2595) - 1), the reference's mixed definitions)."""
+    f32 = np.float32
+    nb = n_fft // 2 + 1
+
+    def h2m(f):
+        f = f32(1.0) if f == 0 else f32(f)
+        return f32(1127.0) * np.log1p(f32(f / f32(700.0)), dtype=np.float32)
+
+    lo, hi = h2m(0.0), h2m(sr // 2)
+    bw = f32(sr) / f32(n_fft)
+    bins = []
+    for i in range(n_filters + 2):
+        m = f32(lo + f32(i) * (hi - lo) / f32(n_filters + 1))
+        hz = f32(700.0) * (np.power(f32(10.0), f32(m / f32(2595.0)), dtype=np.float32) - f32(1.0))
+        bins.append(int(np.floor(f32(hz / bw))))
+    fb = np.zeros((n_filters, nb), np.float32)
+    for i in range(n_filters):
+        l, c, r = (min(max(b, 0), nb - 1) for b in bins[i:i + 3])
+        if l >= c:
+            c = l + 1
+        if c >= r:
+            r = c + 1
+        if r >= nb:
+            r = nb - 1
+        for j in range(l, c + 1):
+            fb[i, j] = f32(j - l) / f32(c - l)
+        for j in range(c, r + 1):
+            fb[i, j] = f32(r - j) / f32(r - c)
+    return fb.T
+
+
+def mfcc_esp(x: np.ndarray, esp_pack: bool = True, frame: int = 320, hop: int = 256, n_fft: int = N_FFT,
+             n_filters: int = N_MELS, n_mfcc: int = N_MFCC) -> np.ndarray:
+    """Mode-A MFCC of one signal (L,) -> (n_frames, n_mfcc), frame-major.
+    float64 DFT (exact) in place of esp-dsp's float radix-2 FFT."""
+    x = np.asarray(x, np.float32)
+    L = x.shape[0]
+    nf = (L - frame) // hop + 1
+    y = np.empty_like(x)
+    y[0] = x[0]
+    y[1:] = x[1:] - np.float32(0.97) * x[:-1]
+    i = np.arange(frame)
+    win = (np.float32(0.53836) - np.float32(1.0 - 0.53836) *
+           np.cos(2.0 * np.pi * i / (frame - 1)).astype(np.float32)).astype(np.float32)
+    idx = np.arange(nf)[:, None] * hop + i[None, :]
+    fr = (y[idx] * win).astype(np.float64)
+    X = np.fft.rfft(fr, n=n_fft, axis=-1)
+    re, im = X.real.astype(np.float32), X.imag.astype(np.float32)
+    if esp_pack:
+        re[:, 1:-1] *= 2.0
+        im[:, 1:-1] *= 2.0
+        re[:, -1] = 0.0
+        im[:, -1] = 0.0
+    pw = (re * re + im * im) / np.float32(n_fft) + np.float32(1e-12)
+    mel = np.log(np.maximum(pw.astype(np.float64) @ fbank_mode_a(n_filters=n_filters, n_fft=n_fft), 1e-12))
+    k = np.arange(n_mfcc)[:, None]
+    n = np.arange(n_filters)[None, :]
+    D = np.cos(np.pi * k * (2 * n + 1) / (2.0 * n_filters))
+    scale = np.where(np.arange(n_mfcc) == 0, np.sqrt(1.0 / n_filters), np.sqrt(2.0 / n_filters))
+    return (mel @ D.T) * scale[None, :]

@@ -108,3 +108,26 @@ def test_generated_mel_tables_match_oracle():
             fb[k, int(m.group(1))] += 4.0 * float(m.group(2))
     ref = O.melscale_fbanks()
     assert np.abs(fb - ref).max() < 1e-5   # torchaudio builds the bank in fp32
+
+
+# ---- front-end mode A (mfcc.c): C restatement vs numpy restatement --------
+def test_mode_a_c_oracle_matches_numpy():
+    from oracle import build_oracle as B
+    x = O.synth_clips(1234, 0, 3, 16000)
+    for pack in (True, False):
+        for i in range(3):
+            a = B.esp_mfcc(x[i], pack)
+            b = O.mfcc_esp(x[i], pack)
+            assert a.shape == b.shape == (62, 13)
+            assert np.abs(a - b).max() <= 2e-5 * np.abs(b).max() + 1e-4
+
+
+def test_mode_a_fbank_and_geometry():
+    from oracle import build_oracle as B
+    fb = B.fbank()
+    assert int((fb != 0).sum()) == 454
+    np.testing.assert_array_equal(fb, O.fbank_mode_a().T)
+    assert B.esp_mfcc(np.zeros(16192, np.float32)).shape == (63, 13)   # hello_world_main.cpp:207-224 length
+    assert B.esp_mfcc(np.ones(320, np.float32)).shape == (1, 13)
+    with pytest.raises(ValueError):
+        B.esp_mfcc(np.ones(319, np.float32))                # signal_len < frame_size -> NULL (mfcc.c:434)
