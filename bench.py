@@ -89,6 +89,7 @@ def main():
     import torch.distributed as dist
     import wakeword
     from wakeword import _lib
+    from wakeword.shard import weak_shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -106,7 +107,8 @@ def main():
 
     B = args.batch
     model = wakeword.load_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"), device=local)
-    clips = wakeword.synth_clips(args.seed, rank * B, B, 16000, device=local)   # resident in HBM
+    first, count = weak_shard(B, rank)                     # per-rank clip split, no collective
+    clips = wakeword.synth_clips(args.seed, first, count, 16000, device=local)   # resident in HBM
     logits = torch.empty((B,), dtype=torch.float32, device=f"cuda:{local}")
     L = _lib.lib()
     h = model._h.h
