@@ -1,0 +1,78 @@
+"""Streaming benchmark, SURVEY 8(d) config 3 (not the driver's bench.py line).
+
+One continuous 16 kHz stream (default 60 s, the device generator's clips laid
+end to end), 1 s windows every 30 ms (hop 480):
+  * latency: the stream is pushed hop by hop through wk_stream_push (host
+    samples -> device ring -> fused kernel on the newest window -> logit on the
+    host); per-push wall time = window available on host -> logit on host.
+    p50 / p90 / p99 reported.
+  * throughput: the whole backlog as one strided launch over the resident
+    stream (clip_stride = hop, overlapping windows), windows/s.
+Prints one JSON line."""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [REPO, os.path.join(REPO, "esp32-wake-word_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=int, default=60)
+    ap.add_argument("--hop", type=int, default=480)
+    ap.add_argument("--backlog-seconds", type=int, default=3600, help="stream length for the throughput leg")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import wakeword
+    from wakeword import _lib
+
+    model = wakeword.load_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"))
+    audio = wakeword.synth_clips(1234, 0, args.seconds).reshape(-1).cpu().numpy()
+    det = wakeword.StreamingDetector(model, hop=args.hop)
+    lat = []
+    for p in range(0, audio.size, args.hop):
+        t0 = time.perf_counter()
+        out = det.push(audio[p:p + args.hop])
+        if out:
+            lat.append(time.perf_counter() - t0)
+    det.close()
+    lat = np.asarray(lat[10:]) * 1e3   # drop warm-up pushes
+
+    # throughput: a long resident stream scored as one backlog of overlapping windows
+    dev = wakeword.synth_clips(1234, 0, args.backlog_seconds).reshape(-1)
+    n = (dev.numel() - 16000) // args.hop + 1
+    logits = torch.empty(n, dtype=torch.float32, device=dev.device)
+    st = torch.cuda.current_stream()
+
+    def run():
+        _lib.check(_lib.lib().wk_forward(model._h.h, C.c_void_p(dev.data_ptr()), _lib.WK_DTYPE_F32, n, 16000,
+                                         args.hop, C.c_void_p(logits.data_ptr()), None,
+                                         C.c_void_p(st.cuda_stream)), "wk_forward")
+    run()
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    thr = n * reps / (time.perf_counter() - t0)
+    print(json.dumps({
+        "metric": "streaming 1 s windows @ 30 ms hop (config 3)",
+        "p50_latency_ms": round(float(np.percentile(lat, 50)), 4),
+        "p90_latency_ms": round(float(np.percentile(lat, 90)), 4),
+        "p99_latency_ms": round(float(np.percentile(lat, 99)), 4),
+        "latency_windows": int(lat.size),
+        "throughput_windows_per_s": round(thr, 1),
+        "throughput_stream_seconds": args.backlog_seconds,
+        "realtime_factor": round(thr * args.hop / 16000.0, 1),
+        "hop": args.hop, "dtype": "f32", "data": "synthetic stream (device generator clips end to end)",
+        "n_gpus": 1}))
+
+
+if __name__ == "__main__":
+    main()

@@ -138,7 +138,7 @@ static wk_status check_audio(const void* d_audio, int32_t dtype, int64_t batch, 
   if (dtype != WK_DTYPE_F32 && dtype != WK_DTYPE_I16) return invalid("bad dtype");
   if (mode_b && win_len != WK_WIN_SAMPLES) return invalid("mode B (torchaudio+CMVN) requires win_len == 16000");
   if (!mode_b && win_len < 320) return invalid("mode A requires win_len >= 320");
-  if (clip_stride < win_len) return invalid("clip_stride < win_len");
+  if (batch > 1 && clip_stride < 1) return invalid("clip_stride < 1");   // < win_len = overlapping (sliding) windows
   return WK_OK;
 }
 
@@ -296,6 +296,142 @@ void analyze_mfcc_range(float* mfcc, int size, const char* label) {
   else
     fprintf(stderr, "E (MFCC) %s MFCC: No valid values\n", label ? label : "");
   fflush(stdout);
+}
+
+// ---------------------------------------------------------------------------
+// Streaming ring.
+//
+// Device ring of `cap` float samples, stored mirrored (sample p at p % cap
+// and p % cap + cap), so every window of <= cap samples is contiguous and a
+// run of consecutive windows is one strided wk_forward launch.  Writes follow
+// ring_buffer.c:57-117 (write_rinbuffer): a push longer than the ring keeps
+// only its newest `cap` samples, older data is overwritten.  Window k covers
+// stream samples [k*hop, k*hop + 16000); a push completes every window whose
+// end it reaches; windows whose start was already overwritten are dropped.
+// ---------------------------------------------------------------------------
+struct wk_stream {
+  wk_handle* h;
+  hipStream_t st;
+  int32_t hop, cap;
+  int64_t total;        // samples pushed since create / reset
+  int64_t next_win;     // index of the next window to score
+  float* d_ring;        // [2*cap]
+  float* d_logits;      // [max_win]
+  float* h_stage;       // pinned [cap]
+  float* h_logits;      // pinned [max_win]
+  int32_t max_win;
+};
+
+wk_status wk_stream_create(wk_handle* h, int32_t hop, int32_t capacity, void* stream, wk_stream** out) {
+  if (!h || !out) return invalid("wk_stream_create: null argument");
+  if (hop < 1 || capacity < WK_WIN_SAMPLES + hop) return invalid("wk_stream_create: need hop >= 1, capacity >= 16000 + hop");
+  if (h->cfg.mode != WK_MODE_TORCHAUDIO_CMVN || !h->d_weights)
+    return invalid("wk_stream_create: needs a mode-B handle with weights");
+  *out = nullptr;
+  return on_device(h->cfg.device, [&]() -> wk_status {
+    wk_stream* s = (wk_stream*)calloc(1, sizeof(wk_stream));
+    if (!s) return WK_ERR_NO_MEMORY;
+    s->h = h;
+    s->st = (hipStream_t)stream;
+    s->hop = hop;
+    s->cap = capacity;
+    s->max_win = (capacity - WK_WIN_SAMPLES) / hop + 1;
+    hipError_t e;
+    if ((e = hipMalloc(&s->d_ring, sizeof(float) * 2 * (size_t)capacity)) != hipSuccess ||
+        (e = hipMalloc(&s->d_logits, sizeof(float) * (size_t)s->max_win)) != hipSuccess ||
+        (e = hipHostMalloc(&s->h_stage, sizeof(float) * (size_t)capacity, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&s->h_logits, sizeof(float) * (size_t)s->max_win, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipMemsetAsync(s->d_ring, 0, sizeof(float) * 2 * (size_t)capacity, s->st)) != hipSuccess) {
+      (void)hipFree(s->d_ring);
+      (void)hipFree(s->d_logits);
+      (void)hipHostFree(s->h_stage);
+      (void)hipHostFree(s->h_logits);
+      free(s);
+      return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_stream_create");
+    }
+    *out = s;
+    return WK_OK;
+  });
+}
+
+wk_status wk_stream_destroy(wk_stream* s) {
+  if (!s) return WK_OK;
+  return on_device(s->h->cfg.device, [&]() -> wk_status {
+    (void)hipStreamSynchronize(s->st);
+    (void)hipFree(s->d_ring);
+    (void)hipFree(s->d_logits);
+    (void)hipHostFree(s->h_stage);
+    (void)hipHostFree(s->h_logits);
+    free(s);
+    return WK_OK;
+  });
+}
+
+wk_status wk_stream_reset(wk_stream* s) {
+  if (!s) return invalid("wk_stream_reset: null stream");
+  s->total = 0;
+  s->next_win = 0;
+  return WK_OK;
+}
+
+wk_status wk_stream_push(wk_stream* s, const float* samples, int64_t n, float* out_logits, int64_t* out_end,
+                         int32_t max_out, int32_t* n_out) {
+  if (!s || !n_out || n < 0 || (n > 0 && !samples) || max_out < 0 || (max_out > 0 && !out_logits))
+    return invalid("wk_stream_push: bad arguments");
+  *n_out = 0;
+  return on_device(s->h->cfg.device, [&]() -> wk_status {
+    hipError_t e = hipStreamSynchronize(s->st);   // the staging buffer may still feed the last push's copy
+    if (e != hipSuccess) return hip_fail(e, "wk_stream_push: sync");
+    const int64_t cap = s->cap;
+    // 1. ring write (overwrite-oldest): only the newest `cap` samples of a long push survive.
+    const int64_t skip = n > cap ? n - cap : 0;
+    const int64_t m = n - skip;
+    if (m > 0) {
+      memcpy(s->h_stage, samples + skip, sizeof(float) * (size_t)m);
+      const int64_t p0 = s->total + skip;
+      int64_t done = 0;
+      while (done < m) {   // at most two segments (wrap), each written twice (mirror)
+        const int64_t pos = (p0 + done) % cap;
+        const int64_t len = m - done < cap - pos ? m - done : cap - pos;
+        for (int mirror = 0; mirror < 2; ++mirror) {
+          e = hipMemcpyAsync(s->d_ring + pos + mirror * cap, s->h_stage + done, sizeof(float) * (size_t)len,
+                             hipMemcpyHostToDevice, s->st);
+          if (e != hipSuccess) return hip_fail(e, "wk_stream_push: H2D");
+        }
+        done += len;
+      }
+    }
+    s->total += n;
+    // 2. windows completed by this push whose start is still in the ring.
+    const int64_t last = s->total >= WK_WIN_SAMPLES ? (s->total - WK_WIN_SAMPLES) / s->hop : -1;
+    int64_t first = s->next_win;
+    const int64_t oldest = s->total > cap ? (s->total - cap + s->hop - 1) / s->hop : 0;
+    if (first < oldest) first = oldest;
+    if (last - first + 1 > max_out) first = last - max_out + 1;   // report the newest max_out
+    s->next_win = last + 1 > s->next_win ? last + 1 : s->next_win;
+    const int64_t k = last - first + 1;
+    if (k <= 0) return WK_OK;
+    // 3. score them: contiguous strided runs in the mirrored ring.
+    int64_t w = first;
+    while (w <= last) {
+      const int64_t off = (w * s->hop) % cap;
+      int64_t run = (2 * cap - WK_WIN_SAMPLES - off) / s->hop + 1;   // windows that fit before the mirror end
+      if (run > last - w + 1) run = last - w + 1;
+      wk_status st = wk_forward(s->h, s->d_ring + off, WK_DTYPE_F32, run, WK_WIN_SAMPLES, s->hop,
+                                s->d_logits + (w - first), nullptr, s->st);
+      if (st != WK_OK) return st;
+      w += run;
+    }
+    if ((e = hipMemcpyAsync(s->h_logits, s->d_logits, sizeof(float) * (size_t)k, hipMemcpyDeviceToHost, s->st)) !=
+            hipSuccess ||
+        (e = hipStreamSynchronize(s->st)) != hipSuccess)
+      return hip_fail(e, "wk_stream_push: D2H");
+    memcpy(out_logits, s->h_logits, sizeof(float) * (size_t)k);
+    if (out_end)
+      for (int64_t i = 0; i < k; ++i) out_end[i] = (first + i) * s->hop + WK_WIN_SAMPLES;
+    *n_out = (int32_t)k;
+    return WK_OK;
+  });
 }
 
 }  // extern "C"

@@ -8,5 +8,6 @@ from ._lib import WakewordError, lib  # noqa: F401
 from .api import (KWSModel, extract_mfcc, load_onnx, load_wav, mfcc, normalize_mfcc, pack_weights,  # noqa: F401
                   pad_audio, synth_clips)
 from .onnx_reader import read_onnx, xiaoa_state_dict  # noqa: F401
+from .stream import DecisionRule, StreamingDetector, Window  # noqa: F401
 
 LightweightKWS = KWSModel

@@ -24,7 +24,7 @@ WK_NUM_WEIGHTS = 40224
 # Every symbol include/wakeword.h declares (checked by tests/test_abi.py).
 EXPORTS = ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_synth_clips", "wk_normalize",
            "wk_status_string", "wk_last_error", "wk_abi_version", "extract_mfcc", "free_mfcc",
-           "analyze_mfcc_range")
+           "analyze_mfcc_range", "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push")
 
 
 class WkConfig(C.Structure):
@@ -57,7 +57,12 @@ def _declare(L):
     L.extract_mfcc.restype = fp
     L.free_mfcc.argtypes = [fp]
     L.analyze_mfcc_range.argtypes = [fp, C.c_int, C.c_char_p]
-    for name in ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_synth_clips", "wk_normalize"):
+    L.wk_stream_create.argtypes = [vp, i32, i32, vp, C.POINTER(vp)]
+    L.wk_stream_destroy.argtypes = [vp]
+    L.wk_stream_reset.argtypes = [vp]
+    L.wk_stream_push.argtypes = [vp, fp, i64, fp, C.POINTER(i64), i32, C.POINTER(i32)]
+    for name in ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_synth_clips", "wk_normalize",
+                 "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push"):
         getattr(L, name).restype = i32
 
 

@@ -78,6 +78,7 @@ wk_status wk_destroy(wk_handle* h);
  * d_audio + i*clip_stride elements (dtype WK_DTYPE_F32 or WK_DTYPE_I16; i16 is
  * scaled by 1/32768 like torchaudio.load).  Mode B requires win_len == 16000
  * and writes CMVN'd features [batch][13][63]; mode A accepts win_len >= 320
+ * (clip_stride may be smaller than win_len: overlapping sliding windows)
  * and writes [batch][n_frames][13] with n_frames = (win_len-320)/256+1. */
 wk_status wk_mfcc(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len,
                   int64_t clip_stride, float* d_feats, void* stream);
@@ -102,6 +103,25 @@ wk_status wk_synth_clips(uint32_t seed, int64_t first, int64_t count, int32_t n,
  * 1 = 'minmax', 2 = 'cmvn', 3 = passthrough. In-place allowed. */
 wk_status wk_normalize(const float* d_in, float* d_out, int64_t batch, int32_t n_coef, int32_t n_time,
                        int32_t method, void* stream);
+
+/* ---- Streaming -------------------------------------
+ * A device ring of `capacity` samples (>= 16000 + hop) fed from host memory,
+ * with ring_buffer.c:57-117's overwrite-oldest semantics (write_rinbuffer).
+ * Window k covers stream samples [k*hop, k*hop + 16000) -- the device's
+ * continuously re-scored 1 s window (esp_wake_word_detector.cpp:52-150 slides
+ * it frame by frame).  wk_stream_push() appends n float samples, scores every
+ * window the push completes (oldest first; windows whose start was already
+ * overwritten are dropped, and when more than max_out complete only the
+ * newest max_out are scored) with the fused path on the handle's device, and
+ * returns their logits and end positions (samples since create/reset) in host
+ * memory.  It blocks until the logits are on the host.  Not thread-safe per
+ * stream object. */
+typedef struct wk_stream wk_stream;
+wk_status wk_stream_create(wk_handle* h, int32_t hop, int32_t capacity, void* stream, wk_stream** out);
+wk_status wk_stream_destroy(wk_stream* s);
+wk_status wk_stream_reset(wk_stream* s);   /* forget history (post-detection reset, detector.cpp:249-256) */
+wk_status wk_stream_push(wk_stream* s, const float* host_samples, int64_t n, float* out_logits, int64_t* out_end,
+                         int32_t max_out, int32_t* n_out);
 
 /* Human-readable text for a status / the last HIP error seen by this thread. */
 const char* wk_status_string(wk_status s);
