@@ -22,7 +22,7 @@ struct wk_handle {
   int fused_exp;         // WAKEWORD_FUSED_EXP: role-isolation timing experiments (wrong logits)
 };
 
-namespace {
+namespace wk {
 
 thread_local std::string g_last_error;
 
@@ -36,17 +36,19 @@ wk_status invalid(const char* what) {
   return WK_ERR_INVALID_ARG;
 }
 
-// Run `body` with the handle's device current; restore the caller's device.
-template <typename F>
-wk_status on_device(int dev, F body) {
-  int old = -1;
-  hipError_t e = hipGetDevice(&old);
-  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-  if (old != dev && (e = hipSetDevice(dev)) != hipSuccess) return hip_fail(e, "hipSetDevice");
-  wk_status s = body();
-  if (old != dev) (void)hipSetDevice(old);
+wk_status fail(wk_status s, const char* what) {
+  g_last_error = what;
   return s;
 }
+
+}  // namespace wk
+
+using wk::g_last_error;
+using wk::hip_fail;
+using wk::invalid;
+using wk::on_device;
+
+namespace {
 
 constexpr int64_t kWorkspaceClips = 16384;
 

@@ -1,0 +1,564 @@
+// wk_ctc.hip -- the GRU-CTC head (ml_models/ctc.py) on gfx950.
+//
+//   audio -> log-mel 80 + global z-score (ctc.py:82-107)
+//         -> Linear 80->128 + LayerNorm + ReLU (ctc.py:125-130)
+//         -> 2-layer bidirectional GRU, H = 128 (ctc.py:133-140)
+//         -> Linear 256->V, log_softmax (ctc.py:143-152)
+//         -> greedy CTC decode (ctc.py:453-471)
+//
+// Kernels:
+//   ctc_mel_kernel        16 frames per 256-thread block: reflect-padded frames
+//                         x periodic Hann(400) into LDS, direct 400-point DFT
+//                         (201 bins) from an LDS sin/cos table, power, HTK mel
+//                         (CSR weights), ln(+1e-8).  VALU-bound.
+//   ctc_zscore_kernel     one block per utterance, two-pass mean / unbiased std.
+//   ctc_encoder_kernel    one wave per frame row, weights in LDS, LayerNorm via
+//                         DPP wave sums.
+//   GEMMs (input projections of both GRU directions, the output layer): plain
+//                         library GEMMs (rocBLAS sgemm).
+//   ctc_gru_kernel        persistent recurrence: one 768-thread block per
+//                         (16 utterances, direction); W_hh lives in VGPRs as
+//                         fp32 MFMA A fragments (2 of the 24 16-row tiles per
+//                         wave); per step 16x16x4 MFMAs against h (LDS), gate
+//                         pre-activations through LDS, gates + state update.
+//   ctc_argmax_kernel     one wave per row: bias, max/argmax (first index),
+//                         log-sum-exp, optional log_softmax output.
+//   ctc_greedy_kernel     one thread per utterance: drop blanks, collapse repeats.
+#include <stdlib.h>
+#include <string.h>
+
+#include <math.h>
+#include <vector>
+
+#include <rocblas/rocblas.h>
+
+#include "wk_cnn_dev.h"
+#include "wk_kernels.h"
+
+using namespace wk;
+
+namespace {
+
+constexpr int kNfft = 400, kHop = 160, kBins = kNfft / 2 + 1, kMels = 80, kH = 128;
+constexpr int kFramesPerBlock = 16;
+
+// ---------------------------------------------------------------------------
+// X1: log-mel
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ctc_mel_kernel(const float* __restrict__ audio, int64_t stride, int n_valid,
+                                                      int n_pad, int T, const int* __restrict__ fb_start,
+                                                      const int* __restrict__ fb_len, const int* __restrict__ fb_off,
+                                                      const float* __restrict__ fb_w, float* __restrict__ feats) {
+  __shared__ float xs[kFramesPerBlock][kNfft];
+  __shared__ float cs[kNfft], sn[kNfft];
+  __shared__ float pw[kFramesPerBlock][kBins + 3];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y;
+  const int t0 = blockIdx.x * kFramesPerBlock;
+  const float* x = audio + b * stride;
+  for (int i = tid; i < kNfft; i += 256) {
+    float s, c;
+    sincospif(2.0f * (float)i / (float)kNfft, &s, &c);
+    cs[i] = c;
+    sn[i] = s;
+  }
+  // frame t covers padded positions [t*160, t*160 + 400) of the centre-padded
+  // (200 each side, reflect) signal; the signal itself is the utterance
+  // zero-padded / trimmed to n_pad samples (ctc.py:85-90).
+  for (int i = tid; i < kFramesPerBlock * kNfft; i += 256) {
+    const int f = i / kNfft, n = i - f * kNfft, t = t0 + f;
+    float v = 0.0f;
+    if (t < T) {
+      int p = t * kHop - kNfft / 2 + n;
+      p = p < 0 ? -p : p;
+      p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
+      v = p < n_valid ? x[p] : 0.0f;
+    }
+    float s, c;
+    sincospif(2.0f * (float)n / (float)kNfft, &s, &c);
+    xs[f][n] = v * (0.5f - 0.5f * c);   // periodic Hann(400)
+  }
+  __syncthreads();
+  // DFT: thread (frame f = tid / 16, bin k = tid % 16 + 16 i)
+  {
+    const int f = tid >> 4, k0 = tid & 15;
+    for (int k = k0; k < kBins; k += 16) {
+      float re = 0.0f, im = 0.0f;
+      int idx = 0;
+      for (int n = 0; n < kNfft; ++n) {
+        const float v = xs[f][n];
+        re = __builtin_fmaf(v, cs[idx], re);
+        im = __builtin_fmaf(-v, sn[idx], im);
+        idx += k;
+        idx = idx >= kNfft ? idx - kNfft : idx;
+      }
+      pw[f][k] = __builtin_fmaf(re, re, im * im);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < kFramesPerBlock * kMels; i += 256) {
+    const int f = i / kMels, m = i - f * kMels, t = t0 + f;
+    if (t >= T) continue;
+    float acc = 0.0f;
+    const int s = fb_start[m], n = fb_len[m], o = fb_off[m];
+    for (int j = 0; j < n; ++j) acc = __builtin_fmaf(pw[f][s + j], fb_w[o + j], acc);
+    feats[(b * T + t) * kMels + m] = logf(acc + 1e-8f);
+  }
+}
+
+__global__ __launch_bounds__(1024) void ctc_zscore_kernel(float* __restrict__ feats, int64_t n_per) {
+  __shared__ float red[16];
+  __shared__ float bc;
+  float* f = feats + (int64_t)blockIdx.x * n_per;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  auto block_sum = [&](float v) -> float {
+    v = wave_sum(v);
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    if (tid == 0) {
+      float s = 0.0f;
+      for (int i = 0; i < 16; ++i) s += red[i];
+      bc = s;
+    }
+    __syncthreads();
+    const float r = bc;
+    __syncthreads();
+    return r;
+  };
+  float s = 0.0f;
+  for (int64_t i = tid; i < n_per; i += 1024) s += f[i];
+  const float mean = block_sum(s) / (float)n_per;
+  float q = 0.0f;
+  for (int64_t i = tid; i < n_per; i += 1024) {
+    const float d = f[i] - mean;
+    q = __builtin_fmaf(d, d, q);
+  }
+  const float sd = sqrtf(block_sum(q) / (float)(n_per - 1));
+  if (!(sd > 0.0f)) return;   // ctc.py:101-104: only when std > 0
+  const float inv = 1.0f / sd;
+  for (int64_t i = tid; i < n_per; i += 1024) f[i] = (f[i] - mean) * inv;
+}
+
+// ---------------------------------------------------------------------------
+// X2a: encoder Linear(80,128) + LayerNorm(128) + ReLU, one wave per row
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ctc_encoder_kernel(const float* __restrict__ in, int64_t rows,
+                                                          const float* __restrict__ w, const float* __restrict__ bias,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* __restrict__ out) {
+  __shared__ float wt[kMels][kH];   // transposed: wt[k][o]
+  __shared__ float xr[4][kMels];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < kMels * kH; i += 256) {
+    const int o = i / kMels, k = i - o * kMels;
+    wt[k][o] = w[i];
+  }
+  const float b0 = bias[lane], b1 = bias[lane + 64];
+  const float g0 = gamma[lane], g1 = gamma[lane + 64], e0 = beta[lane], e1 = beta[lane + 64];
+  __syncthreads();
+  for (int64_t r0 = (int64_t)blockIdx.x * 4; r0 < rows; r0 += (int64_t)gridDim.x * 4) {
+    const int64_t r = r0 + wv;
+    const bool act = r < rows;   // wave-uniform
+    if (act)
+      for (int k = lane; k < kMels; k += 64) xr[wv][k] = in[r * kMels + k];
+    wave_lds_sync();
+    float a0 = b0, a1 = b1;
+    if (act)
+      for (int k = 0; k < kMels; ++k) {
+        const float v = xr[wv][k];
+        a0 = __builtin_fmaf(wt[k][lane], v, a0);
+        a1 = __builtin_fmaf(wt[k][lane + 64], v, a1);
+      }
+    const float mean = wave_sum(a0 + a1) * (1.0f / kH);
+    const float d0 = a0 - mean, d1 = a1 - mean;
+    const float var = wave_sum(d0 * d0 + d1 * d1) * (1.0f / kH);   // biased, as nn.LayerNorm
+    const float rs = 1.0f / sqrtf(var + 1e-5f);
+    if (act) {
+      out[r * kH + lane] = fmaxf(__builtin_fmaf(d0 * rs, g0, e0), 0.0f);
+      out[r * kH + lane + 64] = fmaxf(__builtin_fmaf(d1 * rs, g1, e1), 0.0f);
+    }
+    wave_lds_sync();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// X2b: GRU recurrence (one layer, both directions)
+//   r = s(Wir x + bir + Whr h + bhr), z = s(Wiz x + biz + Whz h + bhz),
+//   n = tanh(Win x + bin + r (Whn h + bhn)), h' = (1 - z) n + z h
+// gi = x W_ih^T for both directions comes precomputed: [B][T][768] (dir*384 + gate*128 + u).
+// ---------------------------------------------------------------------------
+constexpr int kGruBatch = 16, kGruWaves = 12, kGruThreads = 64 * kGruWaves;
+constexpr int kHP = 17;   // LDS pitch of [unit][batch] images (conflict-free for consecutive units)
+
+__device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + __expf(-v)); }
+
+__global__ __launch_bounds__(kGruThreads) void ctc_gru_kernel(const float* __restrict__ gi, const float* __restrict__ whh_pk,
+                                                              const float* __restrict__ bih, const float* __restrict__ bhh,
+                                                              int64_t B, int T, float* __restrict__ out) {
+  __shared__ float hs[2][kH * kHP];
+  __shared__ float gh[3 * kH * kHP];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int dir = blockIdx.y;
+  const int64_t b0 = (int64_t)blockIdx.x * kGruBatch;
+  // W_hh fragments: this wave's tiles 2w, 2w+1 (rows 16 tile .. +15), k-step s covers k = 4s..4s+3.
+  float wa[32], wb[32];
+  {
+    const float* p = whh_pk + ((size_t)dir * 24 + 2 * wave) * 32 * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      wa[s] = p[s * 64];
+      wb[s] = p[(32 + s) * 64];
+    }
+  }
+  for (int i = tid; i < kH * kHP; i += kGruThreads) hs[0][i] = 0.0f;   // h0 = 0
+  __syncthreads();
+  const float* bi = bih + dir * 3 * kH;
+  const float* bh = bhh + dir * 3 * kH;
+  int cur = 0;
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    // gh = W_hh h  (MFMA: A = W rows, B = h[k][n], D rows = gate rows, cols = batch)
+    {
+      f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
+      const float* hb = hs[cur] + (lane >> 4) * kHP + (lane & 15);
+#pragma unroll
+      for (int s = 0; s < 32; ++s) {
+        const float hv = hb[4 * s * kHP];
+        acc_a = mfma4(wa[s], hv, acc_a);
+        acc_b = mfma4(wb[s], hv, acc_b);
+      }
+      const int ra = 32 * wave + 4 * (lane >> 4), col = lane & 15;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gh[(ra + r) * kHP + col] = acc_a[r];
+        gh[(ra + 16 + r) * kHP + col] = acc_b[r];
+      }
+    }
+    __syncthreads();
+    // gates: element e -> (batch n = e / 128, unit u = e % 128): coalesced gi / out rows
+    for (int e = tid; e < kGruBatch * kH; e += kGruThreads) {
+      const int n = e >> 7, u = e & (kH - 1);
+      const int64_t b = b0 + n;
+      float hn = 0.0f;
+      if (b < B) {
+        const float* g = gi + ((size_t)b * T + t) * (6 * kH) + dir * 3 * kH;
+        const float r = sigm(g[u] + bi[u] + gh[u * kHP + n] + bh[u]);
+        const float z = sigm(g[kH + u] + bi[kH + u] + gh[(kH + u) * kHP + n] + bh[kH + u]);
+        const float c = tanhf(g[2 * kH + u] + bi[2 * kH + u] + r * (gh[(2 * kH + u) * kHP + n] + bh[2 * kH + u]));
+        const float hp = hs[cur][u * kHP + n];
+        hn = __builtin_fmaf(z, hp - c, c);   // (1 - z) c + z h
+        out[((size_t)b * T + t) * (2 * kH) + dir * kH + u] = hn;
+      }
+      hs[cur ^ 1][u * kHP + n] = hn;
+    }
+    cur ^= 1;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// X2c / X3: bias + log_softmax + argmax, one wave per row; greedy collapse
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ctc_argmax_kernel(const float* __restrict__ logits, const float* __restrict__ bias,
+                                                         int64_t rows, int V, float* __restrict__ log_probs,
+                                                         int* __restrict__ best) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;   // wave-uniform
+  const float* x = logits + r * V;
+  float mx = -INFINITY;
+  int arg = 0x7fffffff;
+  for (int v = lane; v < V; v += 64) {
+    const float y = x[v] + bias[v];
+    if (y > mx) { mx = y; arg = v; }
+  }
+  for (int m = 32; m >= 1; m >>= 1) {   // max, first index on ties (torch.max)
+    const float om = __shfl_xor(mx, m, 64);
+    const int oa = __shfl_xor(arg, m, 64);
+    if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+  }
+  float s = 0.0f;
+  for (int v = lane; v < V; v += 64) s += __expf(x[v] + bias[v] - mx);
+  const float lse = mx + logf(wave_sum(s));
+  if (log_probs)
+    for (int v = lane; v < V; v += 64) log_probs[r * V + v] = x[v] + bias[v] - lse;
+  if (lane == 0) best[r] = arg;
+}
+
+__global__ void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T, int* __restrict__ tokens,
+                                  int* __restrict__ lengths) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int* p = best + b * T;
+  int* o = tokens + b * T;
+  int prev = 0, n = 0;   // prev starts at the blank (ctc.py:462)
+  for (int t = 0; t < T; ++t) {
+    const int tok = p[t];
+    if (tok != 0 && tok != prev) o[n++] = tok;
+    prev = tok;
+  }
+  for (int t = n; t < T; ++t) o[t] = -1;
+  lengths[b] = n;
+}
+
+// HTK mel filterbank of torchaudio.functional.melscale_fbanks(201, 0, 8000, 80, 16000), in fp32 like torch.
+void mel_fbank(std::vector<float>& fb) {
+  fb.assign((size_t)kBins * kMels, 0.0f);
+  const double m_min = 0.0, m_max = 2595.0 * log10(1.0 + 8000.0 / 700.0);
+  std::vector<float> f_pts(kMels + 2), freqs(kBins);
+  for (int i = 0; i < kMels + 2; ++i) {
+    const float m = (float)(m_min + (m_max - m_min) * i / (kMels + 1));
+    f_pts[i] = 700.0f * (powf(10.0f, m / 2595.0f) - 1.0f);
+  }
+  for (int k = 0; k < kBins; ++k) freqs[k] = (float)(8000.0 * k / (kBins - 1));
+  for (int k = 0; k < kBins; ++k)
+    for (int m = 0; m < kMels; ++m) {
+      const float down = -(f_pts[m] - freqs[k]) / (f_pts[m + 1] - f_pts[m]);
+      const float up = (f_pts[m + 2] - freqs[k]) / (f_pts[m + 2] - f_pts[m + 1]);
+      const float v = fminf(down, up);
+      fb[(size_t)k * kMels + m] = v > 0.0f ? v : 0.0f;
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+struct wk_ctc {
+  wk_ctc_config cfg;
+  rocblas_handle blas;
+  int n_cu;
+  // weights (device)
+  float *enc_w, *enc_b, *ln_g, *ln_b;
+  float* wih[2];        // per layer: [768][Din] (fwd rows then reverse rows)
+  float* bih[2];        // per layer: [768]
+  float* bhh[2];        // per layer: [768]
+  float* whh_pk[2];     // per layer: [2 dir][24 tiles][32 k-steps][64 lanes]
+  float *out_w, *out_b; // [V][256], [V]
+  int *fb_start, *fb_len, *fb_off;
+  float* fb_w;
+  // workspace (grown on demand)
+  size_t ws_rows;
+  float *x0, *gi, *y0, *y1, *logits;
+  int* best;
+};
+
+namespace {
+
+int64_t ctc_num_weights(const wk_ctc_config* c) {
+  const int64_t H = c->hidden, V = c->vocab;
+  int64_t n = H * kMels + 3 * H;
+  for (int l = 0; l < 2; ++l) n += 2 * (3 * H * (l == 0 ? H : 2 * H) + 3 * H * H + 6 * H);
+  return n + V * 2 * H + V;
+}
+
+void free_ws(wk_ctc* c) {
+  (void)hipFree(c->x0);
+  (void)hipFree(c->gi);
+  (void)hipFree(c->y0);
+  (void)hipFree(c->y1);
+  (void)hipFree(c->logits);
+  (void)hipFree(c->best);
+  c->x0 = c->gi = c->y0 = c->y1 = c->logits = nullptr;
+  c->best = nullptr;
+  c->ws_rows = 0;
+}
+
+void free_all(wk_ctc* c) {
+  free_ws(c);
+  float* fs[] = {c->enc_w, c->enc_b, c->ln_g, c->ln_b, c->wih[0], c->wih[1], c->bih[0], c->bih[1], c->bhh[0],
+                 c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->fb_w};
+  for (float* p : fs) (void)hipFree(p);
+  (void)hipFree(c->fb_start);
+  (void)hipFree(c->fb_len);
+  (void)hipFree(c->fb_off);
+  if (c->blas) rocblas_destroy_handle(c->blas);
+}
+
+template <typename T>
+hipError_t upload(T** d, const T* h, size_t n) {
+  hipError_t e = hipMalloc(d, sizeof(T) * n);
+  if (e != hipSuccess) return e;
+  return hipMemcpy(*d, h, sizeof(T) * n, hipMemcpyHostToDevice);
+}
+
+// Row-major C[M][N] = A[M][K] * W[N][K]^T (rocBLAS is column-major: C^T = W * A^T).
+wk_status gemm_nt(rocblas_handle h, int64_t M, int N, int K, const float* A, const float* W, float* C) {
+  const float one = 1.0f, zero = 0.0f;
+  for (int64_t m0 = 0; m0 < M; m0 += (1 << 30) / (N > K ? N : K)) {   // keep every dimension in int range
+    const int64_t m = M - m0 < (1 << 30) / (N > K ? N : K) ? M - m0 : (1 << 30) / (N > K ? N : K);
+    const rocblas_status s = rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, N, (int)m, K, &one,
+                                           W, K, A + m0 * K, K, &zero, C + m0 * N, N);
+    if (s != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_sgemm failed");
+  }
+  return WK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t wk_ctc_num_weights(const wk_ctc_config* cfg) { return cfg ? ctc_num_weights(cfg) : -1; }
+
+wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) {
+  if (!cfg || !w || !out) return invalid("wk_ctc_create: null argument");
+  if (cfg->hidden != kH || cfg->layers != 2 || cfg->n_mels != kMels || cfg->vocab < 2)
+    return fail(WK_ERR_UNSUPPORTED, "wk_ctc_create: this build implements hidden=128, layers=2, n_mels=80, vocab>=2");
+  *out = nullptr;
+  return on_device(cfg->device, [&]() -> wk_status {
+    wk_ctc* c = (wk_ctc*)calloc(1, sizeof(wk_ctc));
+    if (!c) return WK_ERR_NO_MEMORY;
+    c->cfg = *cfg;
+    hipDeviceProp_t prop;
+    c->n_cu = hipGetDeviceProperties(&prop, cfg->device) == hipSuccess ? prop.multiProcessorCount : 256;
+    if (rocblas_create_handle(&c->blas) != rocblas_status_success) {
+      free(c);
+      return fail(WK_ERR_HIP, "rocblas_create_handle failed");
+    }
+    const int H = kH, V = cfg->vocab;
+    const float* p = w;
+    auto take = [&](size_t n) { const float* q = p; p += n; return q; };
+    const float* enc_w = take((size_t)H * kMels);
+    const float* enc_b = take(H);
+    const float* ln_g = take(H);
+    const float* ln_b = take(H);
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = upload(&c->enc_w, enc_w, (size_t)H * kMels);
+    if (e == hipSuccess) e = upload(&c->enc_b, enc_b, H);
+    if (e == hipSuccess) e = upload(&c->ln_g, ln_g, H);
+    if (e == hipSuccess) e = upload(&c->ln_b, ln_b, H);
+    for (int l = 0; l < 2 && e == hipSuccess; ++l) {
+      const int din = l == 0 ? H : 2 * H;
+      std::vector<float> wih(6 * (size_t)H * din), bih(6 * H), bhh(6 * H), pk(2 * 24 * 32 * 64);
+      for (int d = 0; d < 2; ++d) {
+        const float* wi = take(3 * (size_t)H * din);
+        const float* wh = take(3 * (size_t)H * H);
+        const float* bi = take(3 * H);
+        const float* bh = take(3 * H);
+        memcpy(&wih[(size_t)d * 3 * H * din], wi, sizeof(float) * 3 * H * din);
+        memcpy(&bih[d * 3 * H], bi, sizeof(float) * 3 * H);
+        memcpy(&bhh[d * 3 * H], bh, sizeof(float) * 3 * H);
+        for (int tl = 0; tl < 24; ++tl)
+          for (int s = 0; s < 32; ++s)
+            for (int ln = 0; ln < 64; ++ln)
+              pk[(((size_t)d * 24 + tl) * 32 + s) * 64 + ln] = wh[(size_t)(16 * tl + (ln & 15)) * H + 4 * s + (ln >> 4)];
+      }
+      e = upload(&c->wih[l], wih.data(), wih.size());
+      if (e == hipSuccess) e = upload(&c->bih[l], bih.data(), bih.size());
+      if (e == hipSuccess) e = upload(&c->bhh[l], bhh.data(), bhh.size());
+      if (e == hipSuccess) e = upload(&c->whh_pk[l], pk.data(), pk.size());
+    }
+    if (e == hipSuccess) e = upload(&c->out_w, take((size_t)V * 2 * H), (size_t)V * 2 * H);
+    if (e == hipSuccess) e = upload(&c->out_b, take(V), V);
+    // mel filterbank as CSR (per filter: first bin, count, weights)
+    std::vector<float> fb;
+    mel_fbank(fb);
+    std::vector<int> st(kMels), ln(kMels), off(kMels);
+    std::vector<float> wv;
+    for (int m = 0; m < kMels; ++m) {
+      int a = -1, z = -1;
+      for (int k = 0; k < kBins; ++k)
+        if (fb[(size_t)k * kMels + m] != 0.0f) { if (a < 0) a = k; z = k; }
+      if (a < 0) a = z = 0;
+      st[m] = a;
+      ln[m] = z - a + 1;
+      off[m] = (int)wv.size();
+      for (int k = a; k <= z; ++k) wv.push_back(fb[(size_t)k * kMels + m]);
+    }
+    if (e == hipSuccess) e = upload(&c->fb_start, st.data(), kMels);
+    if (e == hipSuccess) e = upload(&c->fb_len, ln.data(), kMels);
+    if (e == hipSuccess) e = upload(&c->fb_off, off.data(), kMels);
+    if (e == hipSuccess) e = upload(&c->fb_w, wv.data(), wv.size());
+    if (e != hipSuccess) {
+      free_all(c);
+      free(c);
+      return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_ctc_create");
+    }
+    *out = c;
+    return WK_OK;
+  });
+}
+
+wk_status wk_ctc_destroy(wk_ctc* c) {
+  if (!c) return WK_OK;
+  return on_device(c->cfg.device, [&]() -> wk_status {
+    (void)hipDeviceSynchronize();
+    free_all(c);
+    free(c);
+    return WK_OK;
+  });
+}
+
+wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n_valid, int32_t n_samples,
+                          int64_t stride, float* d_feats, void* stream) {
+  if (!c || batch < 0 || (batch > 0 && (!d_audio || !d_feats)) || n_samples < kNfft / 2 + 1 || n_valid < 0 ||
+      (batch > 1 && stride < (n_valid < n_samples ? n_valid : n_samples)))
+    return invalid("wk_ctc_features: bad arguments (n_samples must exceed 200 for the reflect pad)");
+  if (batch == 0) return WK_OK;
+  const int T = 1 + n_samples / kHop;
+  return on_device(c->cfg.device, [&]() -> wk_status {
+    hipStream_t st = (hipStream_t)stream;
+    const int nv = n_valid < n_samples ? n_valid : n_samples;
+    for (int64_t b0 = 0; b0 < batch; b0 += 65535) {   // grid.y limit
+      const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+      hipLaunchKernelGGL(ctc_mel_kernel, dim3((T + kFramesPerBlock - 1) / kFramesPerBlock, (unsigned)nb), dim3(256), 0,
+                         st, d_audio + b0 * stride, stride, nv, n_samples, T, c->fb_start, c->fb_len, c->fb_off,
+                         c->fb_w, d_feats + b0 * (int64_t)T * kMels);
+    }
+    hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_features launch");
+  });
+}
+
+wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T, float* d_log_probs,
+                         int32_t* d_tokens, int32_t* d_lengths, void* stream) {
+  if (!c || batch < 0 || T < 1 || (batch > 0 && (!d_feats || !d_tokens || !d_lengths)))
+    return invalid("wk_ctc_forward: bad arguments");
+  if (batch == 0) return WK_OK;
+  const int V = c->cfg.vocab, H = kH;
+  const int64_t rows = batch * (int64_t)T;
+  return on_device(c->cfg.device, [&]() -> wk_status {
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    if ((size_t)rows > c->ws_rows) {   // workspace grows on first use of a larger batch (then reused)
+      if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
+      free_ws(c);
+      if ((e = hipMalloc(&c->x0, sizeof(float) * rows * H)) != hipSuccess ||
+          (e = hipMalloc(&c->gi, sizeof(float) * rows * 6 * H)) != hipSuccess ||
+          (e = hipMalloc(&c->y0, sizeof(float) * rows * 2 * H)) != hipSuccess ||
+          (e = hipMalloc(&c->y1, sizeof(float) * rows * 2 * H)) != hipSuccess ||
+          (e = hipMalloc(&c->logits, sizeof(float) * rows * V)) != hipSuccess ||
+          (e = hipMalloc(&c->best, sizeof(int) * rows)) != hipSuccess) {
+        free_ws(c);
+        return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_ctc_forward workspace");
+      }
+      c->ws_rows = rows;
+    }
+    if (rocblas_set_stream(c->blas, st) != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_set_stream");
+    const int enc_grid = (int)((rows + 3) / 4 < 8 * c->n_cu ? (rows + 3) / 4 : 8 * c->n_cu);
+    hipLaunchKernelGGL(ctc_encoder_kernel, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w, c->enc_b,
+                       c->ln_g, c->ln_b, c->x0);
+    const float* in = c->x0;
+    float* ys[2] = {c->y0, c->y1};
+    for (int l = 0; l < 2; ++l) {
+      wk_status s = gemm_nt(c->blas, rows, 6 * H, l == 0 ? H : 2 * H, in, c->wih[l], c->gi);
+      if (s != WK_OK) return s;
+      hipLaunchKernelGGL(ctc_gru_kernel, dim3((unsigned)((batch + kGruBatch - 1) / kGruBatch), 2), dim3(kGruThreads),
+                         0, st, c->gi, c->whh_pk[l], c->bih[l], c->bhh[l], batch, T, ys[l]);
+      in = ys[l];
+    }
+    wk_status s = gemm_nt(c->blas, rows, V, 2 * H, c->y1, c->out_w, c->logits);
+    if (s != WK_OK) return s;
+    hipLaunchKernelGGL(ctc_argmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits, c->out_b,
+                       rows, V, d_log_probs, c->best);
+    hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st, c->best, batch, T,
+                       d_tokens, d_lengths);
+    e = hipGetLastError();
+    return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_forward launch");
+  });
+}
+
+}  // extern "C"

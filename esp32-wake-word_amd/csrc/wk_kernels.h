@@ -3,7 +3,29 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
+#include "wakeword.h"
+
 namespace wk {
+
+// Error reporting shared by the C-ABI translation units (wk_api.hip, wk_ctc.hip).
+extern thread_local std::string g_last_error;
+wk_status hip_fail(hipError_t e, const char* what);
+wk_status invalid(const char* what);
+wk_status fail(wk_status s, const char* what);
+
+// Run `body` with device `dev` current; restore the caller's device.
+template <typename F>
+wk_status on_device(int dev, F body) {
+  int old = -1;
+  hipError_t e = hipGetDevice(&old);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  if (old != dev && (e = hipSetDevice(dev)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+  wk_status s = body();
+  if (old != dev) (void)hipSetDevice(old);
+  return s;
+}
 
 // Front-end (wk_frontend.hip).  mode_b: torchaudio+CMVN -> [B][13][63];
 // otherwise esp_mfcc -> [B][n_frames][13].

@@ -9,5 +9,6 @@ from .api import (KWSModel, extract_mfcc, load_onnx, load_wav, mfcc, normalize_m
                   pad_audio, synth_clips)
 from .onnx_reader import read_onnx, xiaoa_state_dict  # noqa: F401
 from .stream import DecisionRule, StreamingDetector, Window  # noqa: F401
+from .ctc import CTCModel  # noqa: F401
 
 LightweightKWS = KWSModel

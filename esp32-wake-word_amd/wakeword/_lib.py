@@ -24,12 +24,18 @@ WK_NUM_WEIGHTS = 40224
 # Every symbol include/wakeword.h declares (checked by tests/test_abi.py).
 EXPORTS = ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_synth_clips", "wk_normalize",
            "wk_status_string", "wk_last_error", "wk_abi_version", "extract_mfcc", "free_mfcc",
-           "analyze_mfcc_range", "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push")
+           "analyze_mfcc_range", "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push",
+           "wk_ctc_num_weights", "wk_ctc_create", "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward")
 
 
 class WkConfig(C.Structure):
     _fields_ = [("mode", C.c_int32), ("precision", C.c_int32), ("esp_dsp_packing", C.c_int32),
                 ("device", C.c_int32), ("cmvn", C.c_int32)]
+
+
+class WkCtcConfig(C.Structure):
+    _fields_ = [("vocab", C.c_int32), ("hidden", C.c_int32), ("layers", C.c_int32), ("n_mels", C.c_int32),
+                ("device", C.c_int32)]
 
 
 class WakewordError(RuntimeError):
@@ -62,7 +68,8 @@ def _declare(L):
     L.wk_stream_reset.argtypes = [vp]
     L.wk_stream_push.argtypes = [vp, fp, i64, fp, C.POINTER(i64), i32, C.POINTER(i32)]
     for name in ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_synth_clips", "wk_normalize",
-                 "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push"):
+                 "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push",
+           "wk_ctc_num_weights", "wk_ctc_create", "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward"):
         getattr(L, name).restype = i32
 
 

@@ -21,7 +21,8 @@ CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(PKG, "libwakeword.so")
 OBJDIR = os.path.join(ROOT, "build")
-SOURCES = ["wk_frontend.hip", "wk_cnn.hip", "wk_fused.hip", "wk_misc.hip", "wk_api.hip"]
+SOURCES = ["wk_frontend.hip", "wk_cnn.hip", "wk_fused.hip", "wk_misc.hip", "wk_api.hip", "wk_ctc.hip"]
+LIBS = ["-L/opt/rocm/lib", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]   # rocBLAS: plain GEMMs of the CTC head
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WK_OFFLOAD_ARCH", "gfx950")
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-fno-signed-zeros", "-ffp-contract=fast", "-fno-slp-vectorize",
@@ -56,7 +57,7 @@ def build(force: bool = False, extra=()) -> str:
     with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(lambda s: _compile(s, list(extra)), SOURCES))
     tmp = LIB + ".tmp"
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, *LIBS, "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -123,6 +123,40 @@ wk_status wk_stream_reset(wk_stream* s);   /* forget history (post-detection res
 wk_status wk_stream_push(wk_stream* s, const float* host_samples, int64_t n, float* out_logits, int64_t* out_end,
                          int32_t max_out, int32_t* n_out);
 
+/* ---- CTC head (ml_models/ctc.py) -------------------------
+ * GRU_CTC_Model (ctc.py:119-152) + its log-mel front-end (ctc.py:82-107) +
+ * greedy decode (ctc.py:453-471).  The reference builds V from its corpus at
+ * run time (ctc.py:261-278); here V is a parameter.  This build implements the
+ * reference Config (ctc.py:21-40): hidden 128, 2 bidirectional GRU layers,
+ * 80 mels, n_fft 400, hop 160. */
+typedef struct {
+  int32_t vocab;    /* V, including <blank> = 0 and <unk> = 1                */
+  int32_t hidden;   /* 128 */
+  int32_t layers;   /* 2 */
+  int32_t n_mels;   /* 80 */
+  int32_t device;
+} wk_ctc_config;
+typedef struct wk_ctc wk_ctc;
+
+/* Floats in the weight blob: the GRU_CTC_Model state dict in its own order
+ * (audio_encoder.{0,1}.{weight,bias}, gru.{weight_ih,weight_hh,bias_ih,bias_hh}
+ * _l{0,1}[_reverse], output_layer.{weight,bias}), concatenated. */
+int64_t wk_ctc_num_weights(const wk_ctc_config* cfg);
+wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* host_weights, wk_ctc** out);
+wk_status wk_ctc_destroy(wk_ctc* c);
+/* X1 extract_features: d_audio [batch] rows of float samples (row i at
+ * d_audio + i*stride, n_valid samples each) zero-padded / trimmed to
+ * n_samples (ctc.py:85-90, max_audio_length) -> d_feats [batch][T][80],
+ * T = 1 + n_samples/160, ln(mel+1e-8) z-scored per utterance (ctc.py:95-104). */
+wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n_valid, int32_t n_samples,
+                          int64_t stride, float* d_feats, void* stream);
+/* X2 + X3: d_feats [batch][T][80] -> greedy CTC tokens d_tokens [batch][T]
+ * (blank-free, repeats collapsed, padded with -1) and d_lengths [batch];
+ * d_log_probs_or_null [batch][T][V] receives log_softmax when given.  The
+ * handle's workspace grows on the first call with a larger batch*T. */
+wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T, float* d_log_probs_or_null,
+                         int32_t* d_tokens, int32_t* d_lengths, void* stream);
+
 /* Human-readable text for a status / the last HIP error seen by this thread. */
 const char* wk_status_string(wk_status s);
 const char* wk_last_error(void);

@@ -1,0 +1,85 @@
+"""CTC head (ml_models/ctc.py) through the C ABI against the
+torch-CPU oracle (oracle/wk_ctc_oracle.py: torch.stft restatement of
+torchaudio's MelSpectrogram -- parity unpinned at that boundary -- and the
+torch.nn modules GRU_CTC_Model is built from, with seeded weights; the
+reference ships no trained CTC weights)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import wk_ctc_oracle as CO
+from oracle import wk_oracle as O
+
+FEAT_ATOL = 2e-3      # z-scored log-mel (unit scale)
+LOGP_ATOL = 2e-3      # log_softmax outputs, fp32 end to end
+V = 512
+
+
+def test_greedy_decode_semantics():
+    lp = torch.full((1, 9, 6), -10.0)
+    for t, k in enumerate([0, 3, 3, 0, 3, 5, 5, 1, 1]):
+        lp[0, t, k] = 0.0
+    assert CO.greedy_decode(lp) == [[3, 3, 5, 1]]    # blank separates repeats; prev updated on blanks
+
+
+def test_oracle_feature_shapes_and_zscore():
+    x = torch.from_numpy(O.synth_clips(3, 0, 2, 48000))
+    f = CO.features(x)
+    assert f.shape == (2, 301, 80)
+    assert abs(float(f[0].mean())) < 1e-4 and abs(float(f[0].std()) - 1.0) < 1e-4
+
+
+@pytest.fixture(scope="module")
+def ctc():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    import wakeword
+    m = CO.make_model(V, seed=7)
+    return m, wakeword.CTCModel(CO.flat_weights(m), V)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_valid,n_samples", [(48000, 48000), (30000, 48000), (48000, 128000), (60000, 48000), (400, 480)])
+def test_ctc_features_match_oracle(ctc, n_valid, n_samples):
+    _, g = ctc
+    x = O.synth_clips(11, 0, 5, n_valid)
+    got = g.features(x, n_samples=n_samples).cpu().numpy()
+    ref = CO.features(CO.pad_or_trim(torch.from_numpy(x), n_samples)).numpy()
+    assert got.shape == ref.shape == (5, 1 + n_samples // 160, 80)
+    assert np.abs(got - ref).max() <= FEAT_ATOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 5, 17, 40])
+def test_ctc_forward_matches_oracle(ctc, B):
+    m, g = ctc
+    x = torch.from_numpy(O.synth_clips(5, 0, B, 48000))
+    feats = CO.features(x)
+    with torch.no_grad():
+        ref_lp = m(feats)
+    seqs, lp = g.forward(feats, return_log_probs=True)
+    lp = lp.cpu()
+    assert np.abs((lp - ref_lp).numpy()).max() <= LOGP_ATOL
+    # greedy tokens: identical wherever the oracle's top-2 margin is not a near-tie
+    top2 = torch.topk(ref_lp, 2, dim=-1).values
+    margin = (top2[..., 0] - top2[..., 1]).min().item()
+    if margin > 10 * LOGP_ATOL:
+        assert seqs == CO.greedy_decode(ref_lp)
+    else:
+        ok = (top2[..., 0] - top2[..., 1]) > 10 * LOGP_ATOL
+        assert (lp.argmax(-1) == ref_lp.argmax(-1))[ok].all()
+
+
+@pytest.mark.gpu
+def test_ctc_end_to_end_and_bad_args(ctc):
+    import wakeword
+    m, g = ctc
+    x = O.synth_clips(21, 0, 3, 48000)
+    seqs = g.transcribe(x, n_samples=48000)
+    with torch.no_grad():
+        ref = CO.greedy_decode(m(CO.features(torch.from_numpy(x))))
+    assert len(seqs) == 3 and all(isinstance(s, list) for s in seqs)
+    agree = sum(a == b for a, b in zip(seqs, ref))
+    assert agree >= 2       # near-tie frames may flip one token; see test_ctc_forward_matches_oracle
+    with pytest.raises(ValueError):
+        wakeword.CTCModel(np.zeros(10, np.float32), V)
