@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-utts", type=int, default=8)
+    ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16"],
+                    help="GEMM operand precision (config 5 names fp16; fp32 is the parity mode)")
     args = ap.parse_args()
     import torch
     import wakeword
@@ -31,7 +33,7 @@ def main():
 
     n = args.seconds * 16000
     m = CO.make_model(args.vocab, seed=0)
-    g = wakeword.CTCModel(CO.flat_weights(m), args.vocab)
+    g = wakeword.CTCModel(CO.flat_weights(m), args.vocab, precision=args.precision)
     audio = wakeword.synth_clips(1234, 0, args.batch, n)
     for _ in range(args.warmup):
         g.transcribe(audio, n_samples=n)
@@ -63,7 +65,8 @@ def main():
         "value": round(value, 1), "unit": "utterances/s", "audio_seconds_per_s": round(value * args.seconds, 1),
         "batch": args.batch, "vocab": args.vocab, "T": 1 + n // 160, "steps": args.steps,
         "ms_per_step": round(el / args.steps * 1e3, 3), "frontend_ms": round(t_fe / args.steps, 3),
-        "model_ms": round((t_all - t_fe) / args.steps, 3), "dtype": "f32",
+        "model_ms": round((t_all - t_fe) / args.steps, 3),
+        "dtype": "f32" if args.precision == "fp32" else "f16 GEMM operands / f32 accumulate + recurrence",
         "data": "synthetic (device generator), seeded weights",
         "cpu_baseline": {"value": round(cpu, 2), "unit": "utterances/s", "cores": torch.get_num_threads(),
                          "kind": "port", "sample": f"{args.cpu_utts} utterances, torch-CPU oracle (oracle/wk_ctc_oracle.py)"},

@@ -7,15 +7,16 @@
 //         -> greedy CTC decode (ctc.py:453-471)
 //
 // Kernels:
-//   ctc_mel_kernel        16 frames per 256-thread block: reflect-padded frames
-//                         x periodic Hann(400) into LDS, direct 400-point DFT
-//                         (201 bins) from an LDS sin/cos table, power, HTK mel
-//                         (CSR weights), ln(+1e-8).  VALU-bound.
+//   ctc_frames_kernel     reflect-padded frames x periodic Hann(400) -> [rows][400];
+//                         the 400-point DFT (201 bins) is a GEMM against the
+//                         [402][400] cos/-sin matrix (rocBLAS, fp32);
+//   ctc_power_mel_kernel  power, HTK mel (CSR weights), ln(+1e-8), one wave per frame.
 //   ctc_zscore_kernel     one block per utterance, two-pass mean / unbiased std.
 //   ctc_encoder_kernel    one wave per frame row, weights in LDS, LayerNorm via
 //                         DPP wave sums.
-//   GEMMs (input projections of both GRU directions, the output layer): plain
-//                         library GEMMs (rocBLAS sgemm).
+//   GEMMs (the DFT, input projections of both GRU directions, the output
+//                         layer): plain library GEMMs (rocblas_gemm_ex; fp16
+//                         operands with fp32 accumulation when precision = 1).
 //   ctc_gru_kernel        persistent recurrence: one 768-thread block per
 //                         (16 utterances, direction); W_hh lives in VGPRs as
 //                         fp32 MFMA A fragments (2 of the 24 16-row tiles per
@@ -30,6 +31,7 @@
 #include <math.h>
 #include <vector>
 
+#include <hip/hip_fp16.h>
 #include <rocblas/rocblas.h>
 
 #include "wk_cnn_dev.h"
@@ -40,69 +42,57 @@ using namespace wk;
 namespace {
 
 constexpr int kNfft = 400, kHop = 160, kBins = kNfft / 2 + 1, kMels = 80, kH = 128;
-constexpr int kFramesPerBlock = 16;
 
 // ---------------------------------------------------------------------------
 // X1: log-mel
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ctc_mel_kernel(const float* __restrict__ audio, int64_t stride, int n_valid,
-                                                      int n_pad, int T, const int* __restrict__ fb_start,
-                                                      const int* __restrict__ fb_len, const int* __restrict__ fb_off,
-                                                      const float* __restrict__ fb_w, float* __restrict__ feats) {
-  __shared__ float xs[kFramesPerBlock][kNfft];
-  __shared__ float cs[kNfft], sn[kNfft];
-  __shared__ float pw[kFramesPerBlock][kBins + 3];
-  const int tid = threadIdx.x;
-  const int64_t b = blockIdx.y;
-  const int t0 = blockIdx.x * kFramesPerBlock;
-  const float* x = audio + b * stride;
-  for (int i = tid; i < kNfft; i += 256) {
-    float s, c;
-    sincospif(2.0f * (float)i / (float)kNfft, &s, &c);
-    cs[i] = c;
-    sn[i] = s;
+// Frame t of utterance b covers positions [t*160, t*160 + 400) of the
+// centre-padded (200 each side, reflect) signal, which is itself the
+// utterance zero-padded / trimmed to n_pad samples (ctc.py:85-90).  Writes the
+// Hann-windowed frames, row-major [b*T + t][400], for the DFT GEMM.
+__global__ __launch_bounds__(256) void ctc_frames_kernel(const float* __restrict__ audio, int64_t stride, int n_valid,
+                                                         int n_pad, int T, int64_t rows, float* __restrict__ frames) {
+  const int64_t total = rows * kNfft;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / kNfft;
+    const int n = (int)(i - r * kNfft);
+    const int64_t b = r / T;
+    const int t = (int)(r - b * T);
+    int p = t * kHop - kNfft / 2 + n;
+    p = p < 0 ? -p : p;
+    p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
+    const float v = p < n_valid ? audio[b * stride + p] : 0.0f;
+    float sn, cs;
+    sincospif(2.0f * (float)n / (float)kNfft, &sn, &cs);
+    frames[i] = v * (0.5f - 0.5f * cs);   // periodic Hann(400)
   }
-  // frame t covers padded positions [t*160, t*160 + 400) of the centre-padded
-  // (200 each side, reflect) signal; the signal itself is the utterance
-  // zero-padded / trimmed to n_pad samples (ctc.py:85-90).
-  for (int i = tid; i < kFramesPerBlock * kNfft; i += 256) {
-    const int f = i / kNfft, n = i - f * kNfft, t = t0 + f;
-    float v = 0.0f;
-    if (t < T) {
-      int p = t * kHop - kNfft / 2 + n;
-      p = p < 0 ? -p : p;
-      p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
-      v = p < n_valid ? x[p] : 0.0f;
-    }
-    float s, c;
-    sincospif(2.0f * (float)n / (float)kNfft, &s, &c);
-    xs[f][n] = v * (0.5f - 0.5f * c);   // periodic Hann(400)
-  }
-  __syncthreads();
-  // DFT: thread (frame f = tid / 16, bin k = tid % 16 + 16 i)
-  {
-    const int f = tid >> 4, k0 = tid & 15;
-    for (int k = k0; k < kBins; k += 16) {
-      float re = 0.0f, im = 0.0f;
-      int idx = 0;
-      for (int n = 0; n < kNfft; ++n) {
-        const float v = xs[f][n];
-        re = __builtin_fmaf(v, cs[idx], re);
-        im = __builtin_fmaf(-v, sn[idx], im);
-        idx += k;
-        idx = idx >= kNfft ? idx - kNfft : idx;
+}
+
+// spec [rows][402] = (Re[0..200], Im[0..200]) -> power -> HTK mel -> ln(+1e-8), one wave per row.
+__global__ __launch_bounds__(256) void ctc_power_mel_kernel(const float* __restrict__ spec, int64_t rows,
+                                                            const int* __restrict__ fb_start,
+                                                            const int* __restrict__ fb_len,
+                                                            const int* __restrict__ fb_off,
+                                                            const float* __restrict__ fb_w, float* __restrict__ feats) {
+  __shared__ float pw[4][kBins + 3];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t r0 = (int64_t)blockIdx.x * 4; r0 < rows; r0 += (int64_t)gridDim.x * 4) {
+    const int64_t r = r0 + wv;
+    if (r < rows) {   // wave-uniform
+      const float* x = spec + r * (2 * kBins);
+      for (int k = lane; k < kBins; k += 64) {
+        const float re = x[k], im = x[kBins + k];
+        pw[wv][k] = __builtin_fmaf(re, re, im * im);
       }
-      pw[f][k] = __builtin_fmaf(re, re, im * im);
+      wave_lds_sync();
+      for (int m = lane; m < kMels; m += 64) {
+        float acc = 0.0f;
+        const int s0 = fb_start[m], n = fb_len[m], o = fb_off[m];
+        for (int j = 0; j < n; ++j) acc = __builtin_fmaf(pw[wv][s0 + j], fb_w[o + j], acc);
+        feats[r * kMels + m] = logf(acc + 1e-8f);
+      }
     }
-  }
-  __syncthreads();
-  for (int i = tid; i < kFramesPerBlock * kMels; i += 256) {
-    const int f = i / kMels, m = i - f * kMels, t = t0 + f;
-    if (t >= T) continue;
-    float acc = 0.0f;
-    const int s = fb_start[m], n = fb_len[m], o = fb_off[m];
-    for (int j = 0; j < n; ++j) acc = __builtin_fmaf(pw[f][s + j], fb_w[o + j], acc);
-    feats[(b * T + t) * kMels + m] = logf(acc + 1e-8f);
+    wave_lds_sync();
   }
 }
 
@@ -257,32 +247,156 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru_kernel(const float* __res
   }
 }
 
+// fp16-operand variant (precision 1, config 5): W_hh and h enter
+// v_mfma_f32_16x16x16_f16 as fp16, gate pre-activations accumulate in fp32,
+// gates and the state update stay fp32.  A fragment of tile tl, k-step s:
+// lane l holds W[16 tl + (l & 15)][16 s + 4 (l >> 4) + j], j = 0..3; the B
+// fragment is h16[batch = l & 15][16 s + 4 (l >> 4) + j] from LDS (one b64 read).
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+constexpr int kH16P = kH + 4;   // LDS pitch (halves) of the fp16 state image [batch][unit]
+
+__global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const float* __restrict__ gi, const h4* __restrict__ whh_pk,
+                                                                const float* __restrict__ bih,
+                                                                const float* __restrict__ bhh, int64_t B, int T,
+                                                                float* __restrict__ out) {
+  __shared__ float hs[2][kH * kHP];
+  __shared__ float gh[3 * kH * kHP];
+  __shared__ __attribute__((aligned(16))) _Float16 h16[2][kGruBatch * kH16P];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int dir = blockIdx.y;
+  const int64_t b0 = (int64_t)blockIdx.x * kGruBatch;
+  h4 wa[8], wb[8];
+  {
+    const h4* p = whh_pk + ((size_t)dir * 24 + 2 * wave) * 8 * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      wa[s] = p[s * 64];
+      wb[s] = p[(8 + s) * 64];
+    }
+  }
+  for (int i = tid; i < kH * kHP; i += kGruThreads) hs[0][i] = 0.0f;
+  for (int i = tid; i < kGruBatch * kH16P; i += kGruThreads) h16[0][i] = (_Float16)0.0f;
+  __syncthreads();
+  const float* bi = bih + dir * 3 * kH;
+  const float* bh = bhh + dir * 3 * kH;
+  int cur = 0;
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    {
+      f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
+      const _Float16* hb = h16[cur] + (lane & 15) * kH16P + 4 * (lane >> 4);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const h4 hv = *reinterpret_cast<const h4*>(hb + 16 * s);
+        acc_a = __builtin_amdgcn_mfma_f32_16x16x16f16(wa[s], hv, acc_a, 0, 0, 0);
+        acc_b = __builtin_amdgcn_mfma_f32_16x16x16f16(wb[s], hv, acc_b, 0, 0, 0);
+      }
+      const int ra = 32 * wave + 4 * (lane >> 4), col = lane & 15;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gh[(ra + r) * kHP + col] = acc_a[r];
+        gh[(ra + 16 + r) * kHP + col] = acc_b[r];
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < kGruBatch * kH; e += kGruThreads) {
+      const int n = e >> 7, u = e & (kH - 1);
+      const int64_t b = b0 + n;
+      float hn = 0.0f;
+      if (b < B) {
+        const float* g = gi + ((size_t)b * T + t) * (6 * kH) + dir * 3 * kH;
+        const float r = sigm(g[u] + bi[u] + gh[u * kHP + n] + bh[u]);
+        const float z = sigm(g[kH + u] + bi[kH + u] + gh[(kH + u) * kHP + n] + bh[kH + u]);
+        const float c = tanhf(g[2 * kH + u] + bi[2 * kH + u] + r * (gh[(2 * kH + u) * kHP + n] + bh[2 * kH + u]));
+        const float hp = hs[cur][u * kHP + n];
+        hn = __builtin_fmaf(z, hp - c, c);
+        out[((size_t)b * T + t) * (2 * kH) + dir * kH + u] = hn;
+      }
+      hs[cur ^ 1][u * kHP + n] = hn;
+      h16[cur ^ 1][n * kH16P + u] = (_Float16)hn;
+    }
+    cur ^= 1;
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // X2c / X3: bias + log_softmax + argmax, one wave per row; greedy collapse
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ctc_argmax_kernel(const float* __restrict__ logits, const float* __restrict__ bias,
+// Online softmax state of one lane: running max (first index on ties, as
+// torch.max) and the sum of exp rescaled to it.
+struct SoftmaxAcc {
+  float mx = -INFINITY, s = 0.0f;
+  int arg = 0x7fffffff;
+  __device__ __forceinline__ void push(float y, int v) {
+    if (y > mx) {
+      s = s * __expf(mx - y) + 1.0f;
+      mx = y;
+      arg = v;
+    } else {
+      s += __expf(y - mx);
+    }
+  }
+};
+
+template <typename LT> struct Vec;
+template <> struct Vec<__half> { static constexpr int N = 8; };
+template <> struct Vec<float> { static constexpr int N = 4; };
+
+template <typename LT>
+__global__ __launch_bounds__(256) void ctc_argmax_kernel(const LT* __restrict__ logits, const float* __restrict__ bias,
                                                          int64_t rows, int V, float* __restrict__ log_probs,
                                                          int* __restrict__ best) {
+  constexpr int NV = Vec<LT>::N;   // elements per 16-byte load
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;   // wave-uniform
-  const float* x = logits + r * V;
-  float mx = -INFINITY;
-  int arg = 0x7fffffff;
-  for (int v = lane; v < V; v += 64) {
-    const float y = x[v] + bias[v];
-    if (y > mx) { mx = y; arg = v; }
+  const LT* x = logits + r * V;
+  SoftmaxAcc acc;
+  if (V % NV == 0) {   // rows are 16-byte aligned: one 16-byte load per lane per step
+    for (int c = lane; c < V / NV; c += 64) {
+      LT e[NV];
+      float bb[NV];
+      *reinterpret_cast<uint4*>(e) = reinterpret_cast<const uint4*>(x)[c];
+#pragma unroll
+      for (int q = 0; q < NV / 4; ++q) *reinterpret_cast<float4*>(bb + 4 * q) = reinterpret_cast<const float4*>(bias)[c * (NV / 4) + q];
+      float y[NV];
+      float lm = -INFINITY;
+      int li = 0;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {   // chunk max (first index) ...
+        y[i] = (float)e[i] + bb[i];
+        if (y[i] > lm) { lm = y[i]; li = i; }
+      }
+      float ls = 0.0f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) ls += __expf(y[i] - lm);   // ... independent exps, then one merge
+      if (lm > acc.mx) {
+        acc.s = acc.s * __expf(acc.mx - lm) + ls;
+        acc.mx = lm;
+        acc.arg = c * NV + li;
+      } else {
+        acc.s += ls * __expf(lm - acc.mx);
+      }
+    }
+  } else {
+    for (int v = lane; v < V; v += 64) acc.push((float)x[v] + bias[v], v);
   }
-  for (int m = 32; m >= 1; m >>= 1) {   // max, first index on ties (torch.max)
-    const float om = __shfl_xor(mx, m, 64);
+  float mx = acc.mx, s = acc.s;
+  int arg = acc.arg;
+  for (int m = 32; m >= 1; m >>= 1) {
+    const float om = __shfl_xor(mx, m, 64), os = __shfl_xor(s, m, 64);
     const int oa = __shfl_xor(arg, m, 64);
-    if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+    const float nm = fmaxf(mx, om);
+    s = (mx == -INFINITY ? 0.0f : s * __expf(mx - nm)) + (om == -INFINITY ? 0.0f : os * __expf(om - nm));
+    if (om > mx || (om == mx && oa < arg)) arg = oa;
+    mx = nm;
   }
-  float s = 0.0f;
-  for (int v = lane; v < V; v += 64) s += __expf(x[v] + bias[v] - mx);
-  const float lse = mx + logf(wave_sum(s));
-  if (log_probs)
-    for (int v = lane; v < V; v += 64) log_probs[r * V + v] = x[v] + bias[v] - lse;
+  if (log_probs) {
+    const float lse = mx + logf(s);
+    for (int v = lane; v < V; v += 64) log_probs[r * V + v] = (float)x[v] + bias[v] - lse;
+  }
   if (lane == 0) best[r] = arg;
 }
 
@@ -330,6 +444,7 @@ struct wk_ctc {
   wk_ctc_config cfg;
   rocblas_handle blas;
   int n_cu;
+  bool f16;             // precision 1: GEMM operands in fp16 (fp32 accumulate); recurrence fp32
   // weights (device)
   float *enc_w, *enc_b, *ln_g, *ln_b;
   float* wih[2];        // per layer: [768][Din] (fwd rows then reverse rows)
@@ -337,11 +452,18 @@ struct wk_ctc {
   float* bhh[2];        // per layer: [768]
   float* whh_pk[2];     // per layer: [2 dir][24 tiles][32 k-steps][64 lanes]
   float *out_w, *out_b; // [V][256], [V]
+  __half* wih16[2];     // fp16 copies (precision 1)
+  __half* whh16_pk[2];  // per layer: [2 dir][24 tiles][8 k-steps][64 lanes][4]
+  __half* out_w16;
+  float* dft;           // [402][400]: cos rows k = 0..200, then -sin rows
   int *fb_start, *fb_len, *fb_off;
   float* fb_w;
-  // workspace (grown on demand)
+  // workspaces (grown on demand)
+  size_t fe_rows;
+  float *frames, *spec;
   size_t ws_rows;
   float *x0, *gi, *y0, *y1, *logits;
+  __half *x0h, *y0h, *y1h, *logits16;
   int* best;
 };
 
@@ -355,25 +477,28 @@ int64_t ctc_num_weights(const wk_ctc_config* c) {
 }
 
 void free_ws(wk_ctc* c) {
-  (void)hipFree(c->x0);
-  (void)hipFree(c->gi);
-  (void)hipFree(c->y0);
-  (void)hipFree(c->y1);
-  (void)hipFree(c->logits);
-  (void)hipFree(c->best);
+  void* ps[] = {c->x0, c->gi, c->y0, c->y1, c->logits, c->best, c->x0h, c->y0h, c->y1h, c->logits16};
+  for (void* q : ps) (void)hipFree(q);
   c->x0 = c->gi = c->y0 = c->y1 = c->logits = nullptr;
+  c->x0h = c->y0h = c->y1h = c->logits16 = nullptr;
   c->best = nullptr;
   c->ws_rows = 0;
 }
 
+void free_fe(wk_ctc* c) {
+  (void)hipFree(c->frames);
+  (void)hipFree(c->spec);
+  c->frames = c->spec = nullptr;
+  c->fe_rows = 0;
+}
+
 void free_all(wk_ctc* c) {
   free_ws(c);
-  float* fs[] = {c->enc_w, c->enc_b, c->ln_g, c->ln_b, c->wih[0], c->wih[1], c->bih[0], c->bih[1], c->bhh[0],
-                 c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->fb_w};
-  for (float* p : fs) (void)hipFree(p);
-  (void)hipFree(c->fb_start);
-  (void)hipFree(c->fb_len);
-  (void)hipFree(c->fb_off);
+  free_fe(c);
+  void* ps[] = {c->enc_w, c->enc_b, c->ln_g, c->ln_b, c->wih[0], c->wih[1], c->bih[0], c->bih[1], c->bhh[0],
+                c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->fb_w, c->wih16[0], c->wih16[1],
+                c->out_w16, c->dft, c->fb_start, c->fb_len, c->fb_off, c->whh16_pk[0], c->whh16_pk[1]};
+  for (void* q : ps) (void)hipFree(q);
   if (c->blas) rocblas_destroy_handle(c->blas);
 }
 
@@ -384,16 +509,28 @@ hipError_t upload(T** d, const T* h, size_t n) {
   return hipMemcpy(*d, h, sizeof(T) * n, hipMemcpyHostToDevice);
 }
 
-// Row-major C[M][N] = A[M][K] * W[N][K]^T (rocBLAS is column-major: C^T = W * A^T).
-wk_status gemm_nt(rocblas_handle h, int64_t M, int N, int K, const float* A, const float* W, float* C) {
+hipError_t upload_f16(__half** d, const float* h, size_t n) {
+  std::vector<__half> t(n);
+  for (size_t i = 0; i < n; ++i) t[i] = __float2half(h[i]);
+  return upload(d, t.data(), n);
+}
+
+// Row-major C[M][N] (fp32, or fp16 with c16) = A[M][K] * W[N][K]^T with A, W
+// fp32 or fp16 (fp32 accumulate).  rocBLAS is column-major: C^T = W * A^T.
+wk_status gemm_nt(rocblas_handle h, int64_t M, int64_t N, int64_t K, const void* A, const void* W, void* C, bool f16,
+                  bool c16 = false) {
   const float one = 1.0f, zero = 0.0f;
-  for (int64_t m0 = 0; m0 < M; m0 += (1 << 30) / (N > K ? N : K)) {   // keep every dimension in int range
-    const int64_t m = M - m0 < (1 << 30) / (N > K ? N : K) ? M - m0 : (1 << 30) / (N > K ? N : K);
-    const rocblas_status s = rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, N, (int)m, K, &one,
-                                           W, K, A + m0 * K, K, &zero, C + m0 * N, N);
-    if (s != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_sgemm failed");
-  }
-  return WK_OK;
+  const rocblas_datatype ab = f16 ? rocblas_datatype_f16_r : rocblas_datatype_f32_r;
+  const rocblas_datatype cd = c16 ? rocblas_datatype_f16_r : rocblas_datatype_f32_r;
+  const rocblas_status s = rocblas_gemm_ex_64(h, rocblas_operation_transpose, rocblas_operation_none, N, M, K, &one, W,
+                                              ab, K, A, ab, K, &zero, C, cd, N, C, cd, N, rocblas_datatype_f32_r,
+                                              rocblas_gemm_algo_standard, 0, 0);
+  return s == rocblas_status_success ? WK_OK : fail(WK_ERR_HIP, "rocblas_gemm_ex failed");
+}
+
+__global__ void to_f16_kernel(const float* __restrict__ in, __half* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = __float2half(in[i]);
 }
 
 }  // namespace
@@ -406,11 +543,13 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
   if (!cfg || !w || !out) return invalid("wk_ctc_create: null argument");
   if (cfg->hidden != kH || cfg->layers != 2 || cfg->n_mels != kMels || cfg->vocab < 2)
     return fail(WK_ERR_UNSUPPORTED, "wk_ctc_create: this build implements hidden=128, layers=2, n_mels=80, vocab>=2");
+  if (cfg->precision != 0 && cfg->precision != 1) return invalid("wk_ctc_create: precision must be 0 (fp32) or 1 (fp16)");
   *out = nullptr;
   return on_device(cfg->device, [&]() -> wk_status {
     wk_ctc* c = (wk_ctc*)calloc(1, sizeof(wk_ctc));
     if (!c) return WK_ERR_NO_MEMORY;
     c->cfg = *cfg;
+    c->f16 = cfg->precision == 1;
     hipDeviceProp_t prop;
     c->n_cu = hipGetDeviceProperties(&prop, cfg->device) == hipSuccess ? prop.multiProcessorCount : 256;
     if (rocblas_create_handle(&c->blas) != rocblas_status_success) {
@@ -431,7 +570,7 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     if (e == hipSuccess) e = upload(&c->ln_b, ln_b, H);
     for (int l = 0; l < 2 && e == hipSuccess; ++l) {
       const int din = l == 0 ? H : 2 * H;
-      std::vector<float> wih(6 * (size_t)H * din), bih(6 * H), bhh(6 * H), pk(2 * 24 * 32 * 64);
+      std::vector<float> wih(6 * (size_t)H * din), bih(6 * H), bhh(6 * H), pk(2 * 24 * 32 * 64), pk16(2 * 24 * 8 * 64 * 4);
       for (int d = 0; d < 2; ++d) {
         const float* wi = take(3 * (size_t)H * din);
         const float* wh = take(3 * (size_t)H * H);
@@ -444,28 +583,49 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
           for (int s = 0; s < 32; ++s)
             for (int ln = 0; ln < 64; ++ln)
               pk[(((size_t)d * 24 + tl) * 32 + s) * 64 + ln] = wh[(size_t)(16 * tl + (ln & 15)) * H + 4 * s + (ln >> 4)];
+        for (int tl = 0; tl < 24; ++tl)
+          for (int s = 0; s < 8; ++s)
+            for (int ln = 0; ln < 64; ++ln)
+              for (int j = 0; j < 4; ++j)
+                pk16[((((size_t)d * 24 + tl) * 8 + s) * 64 + ln) * 4 + j] =
+                    wh[(size_t)(16 * tl + (ln & 15)) * H + 16 * s + 4 * (ln >> 4) + j];
       }
       e = upload(&c->wih[l], wih.data(), wih.size());
+      if (e == hipSuccess && c->f16) e = upload_f16(&c->wih16[l], wih.data(), wih.size());
       if (e == hipSuccess) e = upload(&c->bih[l], bih.data(), bih.size());
       if (e == hipSuccess) e = upload(&c->bhh[l], bhh.data(), bhh.size());
       if (e == hipSuccess) e = upload(&c->whh_pk[l], pk.data(), pk.size());
+      if (e == hipSuccess && c->f16) e = upload_f16(&c->whh16_pk[l], pk16.data(), pk16.size());
     }
-    if (e == hipSuccess) e = upload(&c->out_w, take((size_t)V * 2 * H), (size_t)V * 2 * H);
+    const float* ow = take((size_t)V * 2 * H);
+    if (e == hipSuccess) e = upload(&c->out_w, ow, (size_t)V * 2 * H);
+    if (e == hipSuccess && c->f16) e = upload_f16(&c->out_w16, ow, (size_t)V * 2 * H);
     if (e == hipSuccess) e = upload(&c->out_b, take(V), V);
+    // DFT matrix of the 400-point frames: rows k = 0..200 cos(2 pi n k / 400), rows 201.. -sin
+    {
+      std::vector<float> d((size_t)2 * kBins * kNfft);
+      for (int k = 0; k < kBins; ++k)
+        for (int n = 0; n < kNfft; ++n) {
+          const double ang = 2.0 * M_PI * (double)((n * k) % kNfft) / kNfft;
+          d[(size_t)k * kNfft + n] = (float)cos(ang);
+          d[(size_t)(kBins + k) * kNfft + n] = (float)-sin(ang);
+        }
+      if (e == hipSuccess) e = upload(&c->dft, d.data(), d.size());
+    }
     // mel filterbank as CSR (per filter: first bin, count, weights)
     std::vector<float> fb;
     mel_fbank(fb);
     std::vector<int> st(kMels), ln(kMels), off(kMels);
     std::vector<float> wv;
     for (int m = 0; m < kMels; ++m) {
-      int a = -1, z = -1;
+      int a0 = -1, z = -1;
       for (int k = 0; k < kBins; ++k)
-        if (fb[(size_t)k * kMels + m] != 0.0f) { if (a < 0) a = k; z = k; }
-      if (a < 0) a = z = 0;
-      st[m] = a;
-      ln[m] = z - a + 1;
+        if (fb[(size_t)k * kMels + m] != 0.0f) { if (a0 < 0) a0 = k; z = k; }
+      if (a0 < 0) a0 = z = 0;
+      st[m] = a0;
+      ln[m] = z - a0 + 1;
       off[m] = (int)wv.size();
-      for (int k = a; k <= z; ++k) wv.push_back(fb[(size_t)k * kMels + m]);
+      for (int k = a0; k <= z; ++k) wv.push_back(fb[(size_t)k * kMels + m]);
     }
     if (e == hipSuccess) e = upload(&c->fb_start, st.data(), kMels);
     if (e == hipSuccess) e = upload(&c->fb_len, ln.data(), kMels);
@@ -498,17 +658,30 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
     return invalid("wk_ctc_features: bad arguments (n_samples must exceed 200 for the reflect pad)");
   if (batch == 0) return WK_OK;
   const int T = 1 + n_samples / kHop;
+  const int64_t rows = batch * (int64_t)T;
   return on_device(c->cfg.device, [&]() -> wk_status {
     hipStream_t st = (hipStream_t)stream;
-    const int nv = n_valid < n_samples ? n_valid : n_samples;
-    for (int64_t b0 = 0; b0 < batch; b0 += 65535) {   // grid.y limit
-      const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
-      hipLaunchKernelGGL(ctc_mel_kernel, dim3((T + kFramesPerBlock - 1) / kFramesPerBlock, (unsigned)nb), dim3(256), 0,
-                         st, d_audio + b0 * stride, stride, nv, n_samples, T, c->fb_start, c->fb_len, c->fb_off,
-                         c->fb_w, d_feats + b0 * (int64_t)T * kMels);
+    hipError_t e;
+    if ((size_t)rows > c->fe_rows) {
+      if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
+      free_fe(c);
+      if ((e = hipMalloc(&c->frames, sizeof(float) * rows * kNfft)) != hipSuccess ||
+          (e = hipMalloc(&c->spec, sizeof(float) * rows * 2 * kBins)) != hipSuccess) {
+        free_fe(c);
+        return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_ctc_features workspace");
+      }
+      c->fe_rows = rows;
     }
+    if (rocblas_set_stream(c->blas, st) != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_set_stream");
+    const int nv = n_valid < n_samples ? n_valid : n_samples;
+    hipLaunchKernelGGL(ctc_frames_kernel, dim3(16 * c->n_cu), dim3(256), 0, st, d_audio, stride, nv, n_samples, T, rows,
+                       c->frames);
+    wk_status s = gemm_nt(c->blas, rows, 2 * kBins, kNfft, c->frames, c->dft, c->spec, false);   // DFT as a GEMM
+    if (s != WK_OK) return s;
+    hipLaunchKernelGGL(ctc_power_mel_kernel, dim3((unsigned)((rows + 3) / 4 < 16 * c->n_cu ? (rows + 3) / 4 : 16 * c->n_cu)),
+                       dim3(256), 0, st, c->spec, rows, c->fb_start, c->fb_len, c->fb_off, c->fb_w, d_feats);
     hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_features launch");
   });
 }
@@ -520,6 +693,7 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
   if (batch == 0) return WK_OK;
   const int V = c->cfg.vocab, H = kH;
   const int64_t rows = batch * (int64_t)T;
+  const bool f16 = c->f16;
   return on_device(c->cfg.device, [&]() -> wk_status {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
@@ -530,30 +704,52 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
           (e = hipMalloc(&c->gi, sizeof(float) * rows * 6 * H)) != hipSuccess ||
           (e = hipMalloc(&c->y0, sizeof(float) * rows * 2 * H)) != hipSuccess ||
           (e = hipMalloc(&c->y1, sizeof(float) * rows * 2 * H)) != hipSuccess ||
-          (e = hipMalloc(&c->logits, sizeof(float) * rows * V)) != hipSuccess ||
-          (e = hipMalloc(&c->best, sizeof(int) * rows)) != hipSuccess) {
+          (!f16 && (e = hipMalloc(&c->logits, sizeof(float) * rows * V)) != hipSuccess) ||
+          (e = hipMalloc(&c->best, sizeof(int) * rows)) != hipSuccess ||
+          (f16 && (e = hipMalloc(&c->x0h, sizeof(__half) * rows * H)) != hipSuccess) ||
+          (f16 && (e = hipMalloc(&c->y0h, sizeof(__half) * rows * 2 * H)) != hipSuccess) ||
+          (f16 && (e = hipMalloc(&c->y1h, sizeof(__half) * rows * 2 * H)) != hipSuccess) ||
+          (f16 && (e = hipMalloc(&c->logits16, sizeof(__half) * rows * V)) != hipSuccess)) {
         free_ws(c);
         return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_ctc_forward workspace");
       }
       c->ws_rows = rows;
     }
     if (rocblas_set_stream(c->blas, st) != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_set_stream");
+    const int big_grid = 16 * c->n_cu;
     const int enc_grid = (int)((rows + 3) / 4 < 8 * c->n_cu ? (rows + 3) / 4 : 8 * c->n_cu);
     hipLaunchKernelGGL(ctc_encoder_kernel, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w, c->enc_b,
                        c->ln_g, c->ln_b, c->x0);
     const float* in = c->x0;
+    const __half* in16 = c->x0h;
     float* ys[2] = {c->y0, c->y1};
+    __half* ys16[2] = {c->y0h, c->y1h};
     for (int l = 0; l < 2; ++l) {
-      wk_status s = gemm_nt(c->blas, rows, 6 * H, l == 0 ? H : 2 * H, in, c->wih[l], c->gi);
+      const int din = l == 0 ? H : 2 * H;
+      if (f16) hipLaunchKernelGGL(to_f16_kernel, dim3(big_grid), dim3(256), 0, st, in, (__half*)in16, rows * din);
+      wk_status s = f16 ? gemm_nt(c->blas, rows, 6 * H, din, in16, c->wih16[l], c->gi, true)
+                        : gemm_nt(c->blas, rows, 6 * H, din, in, c->wih[l], c->gi, false);
       if (s != WK_OK) return s;
-      hipLaunchKernelGGL(ctc_gru_kernel, dim3((unsigned)((batch + kGruBatch - 1) / kGruBatch), 2), dim3(kGruThreads),
-                         0, st, c->gi, c->whh_pk[l], c->bih[l], c->bhh[l], batch, T, ys[l]);
+      const dim3 gg((unsigned)((batch + kGruBatch - 1) / kGruBatch), 2);
+      if (f16)
+        hipLaunchKernelGGL(ctc_gru16_kernel, gg, dim3(kGruThreads), 0, st, c->gi, (const h4*)c->whh16_pk[l], c->bih[l],
+                           c->bhh[l], batch, T, ys[l]);
+      else
+        hipLaunchKernelGGL(ctc_gru_kernel, gg, dim3(kGruThreads), 0, st, c->gi, c->whh_pk[l], c->bih[l], c->bhh[l],
+                           batch, T, ys[l]);
       in = ys[l];
+      in16 = ys16[l];
     }
-    wk_status s = gemm_nt(c->blas, rows, V, 2 * H, c->y1, c->out_w, c->logits);
+    if (f16) hipLaunchKernelGGL(to_f16_kernel, dim3(big_grid), dim3(256), 0, st, c->y1, c->y1h, rows * 2 * H);
+    wk_status s = f16 ? gemm_nt(c->blas, rows, V, 2 * H, c->y1h, c->out_w16, c->logits16, true, true)
+                      : gemm_nt(c->blas, rows, V, 2 * H, c->y1, c->out_w, c->logits, false);
     if (s != WK_OK) return s;
-    hipLaunchKernelGGL(ctc_argmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits, c->out_b,
-                       rows, V, d_log_probs, c->best);
+    if (f16)   // fp16 logits: half the HBM traffic of the [rows][V] intermediate
+      hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits16,
+                         c->out_b, rows, V, d_log_probs, c->best);
+    else
+      hipLaunchKernelGGL(ctc_argmax_kernel<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits,
+                         c->out_b, rows, V, d_log_probs, c->best);
     hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st, c->best, batch, T,
                        d_tokens, d_lengths);
     e = hipGetLastError();

@@ -35,7 +35,7 @@ class WkConfig(C.Structure):
 
 class WkCtcConfig(C.Structure):
     _fields_ = [("vocab", C.c_int32), ("hidden", C.c_int32), ("layers", C.c_int32), ("n_mels", C.c_int32),
-                ("device", C.c_int32)]
+                ("device", C.c_int32), ("precision", C.c_int32)]
 
 
 class WakewordError(RuntimeError):

@@ -20,12 +20,13 @@ MAX_AUDIO_SAMPLES = 8 * 16000   # Config.max_audio_length (ctc.py:29)
 
 
 class CTCModel:
-    def __init__(self, weights: Union[np.ndarray, Dict[str, np.ndarray]], vocab: int, device: int = 0):
+    def __init__(self, weights: Union[np.ndarray, Dict[str, np.ndarray]], vocab: int, device: int = 0,
+                 precision: str = "fp32"):
         if isinstance(weights, dict):
             weights = np.concatenate([np.asarray(v, np.float32).reshape(-1) for v in weights.values()])
         w = np.ascontiguousarray(weights, np.float32)
         L = lib()
-        self.cfg = _lib.WkCtcConfig(vocab, 128, 2, 80, device)
+        self.cfg = _lib.WkCtcConfig(vocab, 128, 2, 80, device, {"fp32": 0, "fp16": 1}[precision])
         need = L.wk_ctc_num_weights(C.byref(self.cfg))
         if w.size != need:
             raise ValueError(f"expected {need} weights for vocab={vocab}, got {w.size}")

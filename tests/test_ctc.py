@@ -83,3 +83,21 @@ def test_ctc_end_to_end_and_bad_args(ctc):
     assert agree >= 2       # near-tie frames may flip one token; see test_ctc_forward_matches_oracle
     with pytest.raises(ValueError):
         wakeword.CTCModel(np.zeros(10, np.float32), V)
+
+
+@pytest.mark.gpu
+def test_ctc_fp16_gemm_mode(ctc):
+    """precision='fp16' (config 5): GEMM operands in fp16, fp32 accumulation and
+    recurrence -- looser log-prob bound, same decisions on confident frames."""
+    import wakeword
+    m, _ = ctc
+    g16 = wakeword.CTCModel(CO.flat_weights(m), V, precision="fp16")
+    feats = CO.features(torch.from_numpy(O.synth_clips(5, 0, 9, 48000)))
+    with torch.no_grad():
+        ref_lp = m(feats)
+    _, lp = g16.forward(feats, return_log_probs=True)
+    lp = lp.cpu()
+    assert np.abs((lp - ref_lp).numpy()).max() <= 0.05
+    top2 = torch.topk(ref_lp, 2, dim=-1).values
+    ok = (top2[..., 0] - top2[..., 1]) > 0.2
+    assert (lp.argmax(-1) == ref_lp.argmax(-1))[ok].all()
