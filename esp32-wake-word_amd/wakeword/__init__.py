@@ -10,5 +10,6 @@ from .api import (KWSModel, extract_mfcc, load_onnx, load_wav, mfcc, normalize_m
 from .onnx_reader import read_onnx, xiaoa_state_dict  # noqa: F401
 from .stream import DecisionRule, StreamingDetector, Window  # noqa: F401
 from .ctc import CTCModel  # noqa: F401
+from . import wav  # noqa: F401
 
 LightweightKWS = KWSModel

@@ -25,7 +25,8 @@ WK_NUM_WEIGHTS = 40224
 EXPORTS = ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_synth_clips", "wk_normalize",
            "wk_status_string", "wk_last_error", "wk_abi_version", "extract_mfcc", "free_mfcc",
            "analyze_mfcc_range", "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push",
-           "wk_ctc_num_weights", "wk_ctc_create", "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward")
+           "wk_ctc_num_weights", "wk_ctc_create", "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward",
+           "wk_wav_read", "wk_wav_load_batch", "wk_augment")
 
 
 class WkConfig(C.Structure):
@@ -36,6 +37,11 @@ class WkConfig(C.Structure):
 class WkCtcConfig(C.Structure):
     _fields_ = [("vocab", C.c_int32), ("hidden", C.c_int32), ("layers", C.c_int32), ("n_mels", C.c_int32),
                 ("device", C.c_int32), ("precision", C.c_int32)]
+
+
+class WkWavInfo(C.Structure):
+    _fields_ = [("sample_rate", C.c_int32), ("channels", C.c_int32), ("bits_per_sample", C.c_int32),
+                ("data_samples", C.c_int32), ("n_samples", C.c_int32)]
 
 
 class WakewordError(RuntimeError):
@@ -67,9 +73,19 @@ def _declare(L):
     L.wk_stream_destroy.argtypes = [vp]
     L.wk_stream_reset.argtypes = [vp]
     L.wk_stream_push.argtypes = [vp, fp, i64, fp, C.POINTER(i64), i32, C.POINTER(i32)]
+    L.wk_ctc_num_weights.argtypes = [C.POINTER(WkCtcConfig)]
+    L.wk_ctc_num_weights.restype = i64
+    L.wk_ctc_create.argtypes = [C.POINTER(WkCtcConfig), vp, C.POINTER(vp)]
+    L.wk_ctc_destroy.argtypes = [vp]
+    L.wk_ctc_features.argtypes = [vp, vp, i64, i32, i32, i64, vp, vp]
+    L.wk_ctc_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp]
+    L.wk_wav_read.argtypes = [C.c_char_p, vp, i32, C.POINTER(WkWavInfo)]
+    L.wk_wav_load_batch.argtypes = [C.POINTER(C.c_char_p), i32, i32, C.c_float, u32, vp, vp]
+    L.wk_augment.argtypes = [vp, i32, C.c_float, C.c_float, C.c_float, u32, vp, i32]
     for name in ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_synth_clips", "wk_normalize",
-                 "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push",
-           "wk_ctc_num_weights", "wk_ctc_create", "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward"):
+                 "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push", "wk_ctc_create",
+                 "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward", "wk_wav_read", "wk_wav_load_batch",
+                 "wk_augment"):
         getattr(L, name).restype = i32
 
 

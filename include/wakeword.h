@@ -160,6 +160,31 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
 wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T, float* d_log_probs_or_null,
                          int32_t* d_tokens, int32_t* d_lengths, void* stream);
 
+/* ---- WAV ingest and waveform augmentation (host only) ---
+ * No device work: these fill caller (e.g. pinned) host buffers for the H2D copy. */
+typedef struct {
+  int32_t sample_rate, channels, bits_per_sample;
+  int32_t data_samples;   /* frames in the data chunk              */
+  int32_t n_samples;      /* frames actually read (<= max_samples) */
+} wk_wav_info;
+/* esp_wav.cpp:8-139: RIFF/WAVE/"fmt " header, unknown chunks before "data"
+ * skipped, PCM 16-bit only (WK_ERR_UNSUPPORTED otherwise); channel 0 of up
+ * to max_samples frames into out (the reference truncates to 16000). */
+wk_status wk_wav_read(const char* path, int16_t* out, int32_t max_samples, wk_wav_info* info);
+/* torchaudio.load scaling (x/32768) + pad_audio (extract_mfcc.py:7-23) for n
+ * files on worker threads: out[n][pad_to], right-padded with N(0,
+ * noise_level^2) from a counter-hash generator keyed on (seed, file index)
+ * (distribution of torch.randn * noise_level, not its bit stream), or zeros
+ * when noise_level == 0.  n_read[i] (may be NULL) gets each file's length. */
+wk_status wk_wav_load_batch(const char* const* paths, int32_t n, int32_t pad_to, float noise_level, uint32_t seed,
+                            float* out, int32_t* n_read);
+/* augment_audio_waveform (extract_mfcc.py:90-121): speed change by linear
+ * interpolation to int(n*speed) samples (F.interpolate, align_corners=False),
+ * padded (noise as above, stream 0) / trimmed to out_len, then x volume with
+ * clamp to [-1, 1] when volume != 1. */
+wk_status wk_augment(const float* in, int32_t n, float speed, float volume, float noise_level, uint32_t seed, float* out,
+                     int32_t out_len);
+
 /* Human-readable text for a status / the last HIP error seen by this thread. */
 const char* wk_status_string(wk_status s);
 const char* wk_last_error(void);

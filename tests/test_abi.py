@@ -79,3 +79,13 @@ def test_pack_weights_layout(xiaoa_sd):
     assert blob.size == 40224 and blob.dtype.name == "float32"
     assert blob[0] == xiaoa_sd["conv_layers.0.weight"].reshape(-1)[0]
     assert blob[-1] == xiaoa_sd["classifier.2.weight"].reshape(-1)[-1]
+
+
+def test_every_export_has_a_ctypes_prototype(L):
+    """The Python binding declares argument types for every C entry point (an
+    undeclared prototype silently truncates int64 / float arguments)."""
+    from wakeword import _lib
+    no_args = {"wk_last_error", "wk_abi_version"}
+    for name in _lib.EXPORTS:
+        if name not in no_args:
+            assert getattr(L, name).argtypes is not None, name
