@@ -17,6 +17,7 @@ struct wk_handle {
   float* d_weights;      // packed WK_NUM_WEIGHTS floats, or nullptr (front-end only handle)
   float* d_packed;       // fragment-major weights (wk::pack_fragments) for the fused kernel
   float* d_feats_ws;     // feature workspace for the unfused path
+  int8_t* d_int8;        // int8 weights (WK_PREC_INT8, wk::quantize_int8_weights)
   int64_t ws_clips;
   int unfused;           // WAKEWORD_UNFUSED=1: front-end + CNN as two kernels (A/B testing)
   int fused_exp;         // WAKEWORD_FUSED_EXP: role-isolation timing experiments (wrong logits)
@@ -75,7 +76,8 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
   if (!cfg || !out) return invalid("wk_create: null cfg/out");
   *out = nullptr;
   if (cfg->mode != WK_MODE_TORCHAUDIO_CMVN && cfg->mode != WK_MODE_ESP_MFCC) return invalid("wk_create: bad mode");
-  if (cfg->precision != WK_PREC_FP32 && cfg->precision != WK_PREC_BF16) return invalid("wk_create: bad precision");
+  if (cfg->precision != WK_PREC_FP32 && cfg->precision != WK_PREC_BF16 && cfg->precision != WK_PREC_INT8)
+    return invalid("wk_create: bad precision");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
@@ -107,6 +109,13 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
       if ((e2 = hipMemcpy(h->d_packed, pk.data(), sizeof(float) * wk::kNumPacked, hipMemcpyHostToDevice)) !=
           hipSuccess)
         return hip_fail(e2, "hipMemcpy(packed weights)");
+      if (cfg->precision == WK_PREC_INT8) {
+        std::vector<int8_t> q(wk::kNumInt8Weights);
+        wk::quantize_int8_weights(host_weights, q.data());
+        if ((e2 = hipMalloc(&h->d_int8, q.size())) != hipSuccess) return hip_fail(e2, "hipMalloc(int8 weights)");
+        if ((e2 = hipMemcpy(h->d_int8, q.data(), q.size(), hipMemcpyHostToDevice)) != hipSuccess)
+          return hip_fail(e2, "hipMemcpy(int8 weights)");
+      }
       h->ws_clips = kWorkspaceClips;
       if ((e2 = hipMalloc(&h->d_feats_ws, sizeof(float) * 13 * 63 * h->ws_clips)) != hipSuccess)
         return hip_fail(e2, "hipMalloc(workspace)");
@@ -127,6 +136,7 @@ wk_status wk_destroy(wk_handle* h) {
     if (h->d_weights) (void)hipFree(h->d_weights);
     if (h->d_feats_ws) (void)hipFree(h->d_feats_ws);
     if (h->d_packed) (void)hipFree(h->d_packed);
+    if (h->d_int8) (void)hipFree(h->d_int8);
     return WK_OK;
   });
   free(h);
@@ -167,7 +177,9 @@ wk_status wk_cnn(wk_handle* h, const float* d_feats, int64_t batch, float* d_log
     return WK_ERR_UNSUPPORTED;
   }
   return on_device(h->cfg.device, [&]() -> wk_status {
-    hipError_t e = wk::launch_cnn(d_feats, batch, h->d_weights, d_logits, false, h->n_cu, (hipStream_t)stream);
+    hipError_t e = h->cfg.precision == WK_PREC_INT8
+                       ? wk::launch_int8_cnn(d_feats, batch, h->d_int8, d_logits, 4 * h->n_cu, (hipStream_t)stream)
+                       : wk::launch_cnn(d_feats, batch, h->d_weights, d_logits, false, h->n_cu, (hipStream_t)stream);
     return e == hipSuccess ? WK_OK : hip_fail(e, "cnn launch");
   });
 }
@@ -187,8 +199,9 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
     g_last_error = "bf16 CNN not implemented in this build";
     return WK_ERR_UNSUPPORTED;
   }
+  const bool int8 = h->cfg.precision == WK_PREC_INT8;
   return on_device(h->cfg.device, [&]() -> wk_status {
-    if (!h->unfused) {
+    if (!h->unfused && !int8) {
       hipError_t e = wk::launch_fused(dtype == WK_DTYPE_I16, d_audio, batch, clip_stride, h->d_packed, d_logits,
                                       d_feats_or_null, h->n_cu, (hipStream_t)stream, h->fused_exp);
       return e == hipSuccess ? WK_OK : hip_fail(e, "fused launch");
@@ -201,7 +214,8 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
       hipError_t e = wk::launch_frontend(true, dtype == WK_DTYPE_I16, a, n, win_len, clip_stride, feats, 0, 1,
                                          2 * h->n_cu, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(e, "frontend launch");
-      e = wk::launch_cnn(feats, n, h->d_weights, d_logits + c0, false, h->n_cu, (hipStream_t)stream);
+      e = int8 ? wk::launch_int8_cnn(feats, n, h->d_int8, d_logits + c0, 4 * h->n_cu, (hipStream_t)stream)
+               : wk::launch_cnn(feats, n, h->d_weights, d_logits + c0, false, h->n_cu, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(e, "cnn launch");
     }
     return WK_OK;

@@ -43,6 +43,12 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
                         float* logits, float* feats_or_null, int grid_cap, hipStream_t stream,
                         int exp_flags = 0);   // exp_flags (timing experiments only): 1 = FE role only, 2 = CNN only
 
+// int8 CNN in the device's esp-dl arithmetic (wk_int8.hip); feats [B][13][63] fp32.
+constexpr int kNumInt8Weights = 3 * 13 * 32 + 3 * 32 * 64 + 3 * 64 * 128 + 128 * 64 + 64;
+hipError_t launch_int8_cnn(const float* feats, int64_t batch, const int8_t* wq, float* logits, int grid_cap,
+                           hipStream_t stream);
+void quantize_int8_weights(const float* w, int8_t* q);
+
 // Misc (wk_misc.hip).
 hipError_t launch_synth(uint32_t seed, int64_t first, int64_t count, int n, float* out, hipStream_t stream);
 hipError_t launch_normalize(const float* in, float* out, int64_t batch, int n_coef, int n_time, int method,

@@ -44,7 +44,11 @@ typedef enum {
 } wk_mode;
 
 typedef enum { WK_DTYPE_F32 = 0, WK_DTYPE_I16 = 1 } wk_dtype;   /* audio sample type */
-typedef enum { WK_PREC_FP32 = 0, WK_PREC_BF16 = 1 } wk_precision; /* CNN arithmetic    */
+/* CNN arithmetic.  INT8 = the device's esp-dl int8 network (power-of-2
+ * per-tensor exponents of ml_models/xiaoa.info, round-half-even requant;
+ * reproduces the xiaoa.info known-answer test exactly): a device-faithful
+ * checking mode, run unfused after the fp32 front-end. */
+typedef enum { WK_PREC_FP32 = 0, WK_PREC_BF16 = 1, WK_PREC_INT8 = 2 } wk_precision;
 
 typedef struct {
   int32_t mode;            /* wk_mode                                               */

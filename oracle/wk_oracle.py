@@ -297,3 +297,46 @@ def mfcc_esp(x: np.ndarray, esp_pack: bool = True, frame: int = 320, hop: int = 
     D = np.cos(np.pi * k * (2 * n + 1) / (2.0 * n_filters))
     scale = np.where(np.arange(n_mfcc) == 0, np.sqrt(1.0 / n_filters), np.sqrt(2.0 / n_filters))
     return (mel @ D.T) * scale[None, :]
+
+
+# --------------------------------------------------------------------------
+# int8 CNN in the device's esp-dl arithmetic:
+# power-of-2 per-tensor exponents of ml_models/xiaoa.info:3139-3150,
+# weights rne(w * 2^-e) (pinned: equal to xiaoa.info's int8 weights), requant
+# round-half-even (pinned only by the xiaoa.info KAT: test input -> -40).
+# --------------------------------------------------------------------------
+INT8_W_EXP = {"conv_layers.0.weight": -8, "conv_layers.3.weight": -9, "conv_layers.6.weight": -9,
+              "classifier.0.weight": -9, "classifier.2.weight": -9}
+
+
+def quantize_int8(w: dict) -> dict:
+    return {k: np.clip(np.round(np.asarray(w[k], np.float64) * 2.0 ** (-e)), -128, 127).astype(np.int64)
+            for k, e in INT8_W_EXP.items()}
+
+
+def _rne_shift(acc: np.ndarray, s: int) -> np.ndarray:
+    return np.clip(np.round(acc / float(1 << s)), -128, 127).astype(np.int64)   # exact in float64 (|acc| < 2^31)
+
+
+def kws_forward_int8(q_in: np.ndarray, qw: dict) -> np.ndarray:
+    """q_in (B, 13, 63) int8 at exp -4 -> int8 logits (B,) at exp -3."""
+    x = np.asarray(q_in, np.int64)
+
+    def conv(a, W):   # a (B, Cin, T), W (Cout, Cin, 3)
+        T = a.shape[-1]
+        ap = np.pad(a, ((0, 0), (0, 0), (1, 1)))
+        return sum(np.einsum("oc,bct->bot", W[:, :, k], ap[:, :, k:k + T]) for k in range(3))
+
+    for key, s in (("conv_layers.0.weight", 7), ("conv_layers.3.weight", 9), ("conv_layers.6.weight", 10)):
+        x = np.maximum(_rne_shift(conv(x, qw[key]), s), 0)
+        T = x.shape[-1] // 2
+        x = np.maximum(x[..., 0:2 * T:2], x[..., 1:2 * T:2])
+    g = np.clip(np.round(x.sum(-1) * 2.0 / 7.0), -128, 127).astype(np.int64)   # GAP, exp -4 -> -5
+    h = np.maximum(_rne_shift(g @ qw["classifier.0.weight"].T, 10), 0)
+    return _rne_shift(h @ qw["classifier.2.weight"].T, 10)[:, 0]
+
+
+def quantize_input(feats: np.ndarray) -> np.ndarray:
+    """TensorBase::assign float -> int8 at exp -4 (round half away from zero, saturate)."""
+    v = np.asarray(feats, np.float64) * 16.0
+    return np.clip(np.sign(v) * np.floor(np.abs(v) + 0.5), -128, 127).astype(np.int64)

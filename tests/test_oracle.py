@@ -131,3 +131,19 @@ def test_mode_a_fbank_and_geometry():
     assert B.esp_mfcc(np.ones(320, np.float32)).shape == (1, 13)
     with pytest.raises(ValueError):
         B.esp_mfcc(np.ones(319, np.float32))                # signal_len < frame_size -> NULL (mfcc.c:434)
+
+
+def test_int8_oracle_reproduces_the_kat(golden_dir, xiaoa_sd):
+    """xiaoa.info's int8 known-answer test: input (exp -4) -> -40 (exp -3)."""
+    k = np.load(os.path.join(golden_dir, "kat.npz"))
+    q_in = k["kat_in_int8"][0].T[None].astype(np.int64)          # (1, 13, 63)
+    out = O.kws_forward_int8(q_in, O.quantize_int8(xiaoa_sd))
+    assert int(out[0]) == int(k["kat_out_int8"].reshape(-1)[0]) == -40
+
+
+def test_int8_tracks_fp32_on_golden_wavs(golden_dir, xiaoa_sd):
+    w = np.load(os.path.join(golden_dir, "wavs.npz"))
+    f = w["feat_zero"]
+    q = O.kws_forward_int8(O.quantize_input(f), O.quantize_int8(xiaoa_sd)) * 0.125
+    ref = O.kws_forward(f, xiaoa_sd)[:, 0]
+    assert np.abs(q - ref).max() < 1.0                            # int8 vs fp32 logit, exp -3 grid
