@@ -163,7 +163,8 @@ wk_status wk_mfcc(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batc
   if (batch > 0 && !d_feats) return invalid("wk_mfcc: null feats");
   return on_device(h->cfg.device, [&]() -> wk_status {
     hipError_t e = wk::launch_frontend(mode_b, dtype == WK_DTYPE_I16, d_audio, batch, win_len, clip_stride, d_feats,
-                                       h->cfg.esp_dsp_packing, h->cfg.cmvn, 2 * h->n_cu, (hipStream_t)stream);
+                                       h->cfg.esp_dsp_packing, h->cfg.cmvn, 2 * h->n_cu, 0.97f,
+                                       (hipStream_t)stream);
     return e == hipSuccess ? WK_OK : hip_fail(e, "frontend launch");
   });
 }
@@ -212,7 +213,7 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
       float* feats = d_feats_or_null ? d_feats_or_null + c0 * 13 * 63 : h->d_feats_ws;
       const void* a = (const char*)d_audio + (size_t)(c0 * clip_stride) * esz;
       hipError_t e = wk::launch_frontend(true, dtype == WK_DTYPE_I16, a, n, win_len, clip_stride, feats, 0, 1,
-                                         2 * h->n_cu, (hipStream_t)stream);
+                                         2 * h->n_cu, 0.97f, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(e, "frontend launch");
       e = int8 ? wk::launch_int8_cnn(feats, n, h->d_int8, d_logits + c0, 4 * h->n_cu, (hipStream_t)stream)
                : wk::launch_cnn(feats, n, h->d_weights, d_logits + c0, false, h->n_cu, (hipStream_t)stream);
@@ -292,6 +293,59 @@ float* extract_mfcc(const float* signal, int signal_len, int sampling_rate, int 
 }
 
 void free_mfcc(float* mfcc) { free(mfcc); }
+
+// mfcc.c:297-427 flow_extract_mfcc_single_frame: one frame, NO pre-emphasis,
+// symmetric Hamming over frame_size, |FFT|^2/n_fft + 1e-12 (esp-dsp packing),
+// mel, ln, DCT-II -> malloc'd n_mfcc floats (free with free_mfcc), NULL on bad
+// arguments (mfcc.c:300-303).  GPU-backed like extract_mfcc; the reference
+// configuration (320-sample frame, 16 kHz, 512, 40 filters, n_mfcc <= 13) only.
+float* flow_extract_mfcc_single_frame(const float* frame, int frame_size, int sampling_rate, int n_fft, int n_filters,
+                                      int n_mfcc) {
+  if (!frame || frame_size <= 0 || frame_size > n_fft) {
+    fprintf(stderr, "E (MFCC) Invalid frame parameters\n");
+    return nullptr;
+  }
+  if (sampling_rate != 16000 || frame_size != 320 || n_fft != 512 || n_filters != 40 || n_mfcc < 1 || n_mfcc > 13) {
+    fprintf(stderr, "E (MFCC) unsupported configuration (supported: 320-sample frame, 16000/512/40, n_mfcc <= 13)\n");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(g_compat_mu);
+  if (!g_compat) {
+    wk_config cfg = {WK_MODE_ESP_MFCC, WK_PREC_FP32, 1, 0, 0};
+    if (wk_create(&cfg, nullptr, &g_compat) != WK_OK) {
+      fprintf(stderr, "E (MFCC) device init failed: %s\n", wk_last_error());
+      return nullptr;
+    }
+  }
+  float* host_out = (float*)malloc(sizeof(float) * (size_t)n_mfcc);
+  if (!host_out) return nullptr;
+  float tmp[13];
+  float *d_sig = nullptr, *d_out = nullptr;
+  wk_status st = on_device(0, [&]() -> wk_status {
+    hipError_t e;
+    if ((e = hipMalloc(&d_sig, sizeof(float) * frame_size)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if ((e = hipMalloc(&d_out, sizeof(float) * 13)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if ((e = hipMemcpy(d_sig, frame, sizeof(float) * frame_size, hipMemcpyHostToDevice)) != hipSuccess)
+      return hip_fail(e, "H2D");
+    if ((e = wk::launch_frontend(false, false, d_sig, 1, frame_size, frame_size, d_out, 1, 0, 1, 0.0f, nullptr)) !=
+        hipSuccess)
+      return hip_fail(e, "frontend launch");
+    if ((e = hipMemcpy(tmp, d_out, sizeof(float) * 13, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "D2H");
+    return WK_OK;
+  });
+  on_device(0, [&]() -> wk_status {
+    if (d_sig) (void)hipFree(d_sig);
+    if (d_out) (void)hipFree(d_out);
+    return WK_OK;
+  });
+  if (st != WK_OK) {
+    fprintf(stderr, "E (MFCC) flow_extract_mfcc_single_frame failed: %s\n", wk_last_error());
+    free(host_out);
+    return nullptr;
+  }
+  memcpy(host_out, tmp, sizeof(float) * (size_t)n_mfcc);
+  return host_out;
+}
 
 // mfcc.c:530-553: min/max/avg over the finite entries.
 void analyze_mfcc_range(float* mfcc, int size, const char* label) {

@@ -101,7 +101,7 @@ struct FeTables {
 // each sample with the NEXT one: own x1 for y0, the next lane's x0 for y1.
 template <bool MODE_B, typename T>
 __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, int j, bool general,
-                                          const FeTables& tb, f2 (&a)[16] WK_SP_PARAM) {
+                                          const FeTables& tb, f2 (&a)[16], float pre = -0.97f WK_SP_PARAM) {
   float prev_rot = 0.0f;
 #pragma unroll
   for (int n1 = 0; n1 < 10; ++n1) {
@@ -113,8 +113,8 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
     asm volatile("" : "+v"(rot));
     const float xm = j != 0 ? rot : (n1 == 0 ? to_f(raw.xb) : prev_rot);
     prev_rot = rot;
-    float y0 = __builtin_fmaf(-0.97f, xm, x0);
-    float y1 = __builtin_fmaf(-0.97f, x0, x1);
+    float y0 = __builtin_fmaf(pre, xm, x0);   // pre = -0.97 (0 for mfcc.c's single-frame variant)
+    float y1 = __builtin_fmaf(pre, x0, x1);
     if (MODE_B && general) {
       const int i0 = base + 32 * n1 + 2 * j;
       float nx = row_rol1(x0);
@@ -122,7 +122,7 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
       asm volatile("" : "+v"(nx), "+v"(nx1));
       const float xn = j != 15 ? nx : (n1 < 9 ? nx1 : to_f(raw.xb));
       const bool reflected = i0 < 0 || i0 > n - 1;
-      const float r0 = __builtin_fmaf(-0.97f, x1, x0), r1 = __builtin_fmaf(-0.97f, xn, x1);
+      const float r0 = __builtin_fmaf(pre, x1, x0), r1 = __builtin_fmaf(pre, xn, x1);
       y0 = reflected ? r0 : (i0 == 0 ? x0 : y0);
       y1 = reflected ? r1 : y1;
     }

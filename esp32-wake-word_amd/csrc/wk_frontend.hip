@@ -37,7 +37,7 @@ template <bool MODE_B, typename T>
 __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __restrict__ audio, int64_t n_units,
                                                                   int n_chunks, int nf, int win_len,
                                                                   int64_t clip_stride, float* __restrict__ out,
-                                                                  int esp_pack, int cmvn) {
+                                                                  int esp_pack, int cmvn, float pre) {
   __shared__ __attribute__((aligned(16))) float smem[kFeLds];
   float* P = smem + kPOff;
   float* L = smem + kLOff;
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
       frame_of(u, r, t, fl, nfc_r, slow, xp);
       f2 a[16];
       if (fl < nfc) {
-        fe_stage0<MODE_B>(pf, MODE_B ? 256 * t - 160 : 256 * t, win_len, j, slow, tb, a);
+        fe_stage0<MODE_B>(pf, MODE_B ? 256 * t - 160 : 256 * t, win_len, j, slow, tb, a, pre);
       }
       // pf is consumed: prefetch the next wave-round, (u,1) or (u+grid,0), into it.
       prefetch(r == 0 ? u : u + gridDim.x, r ^ 1, pf);
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
 namespace wk {
 
 hipError_t launch_frontend(bool mode_b, bool i16, const void* audio, int64_t batch, int win_len,
-                           int64_t clip_stride, float* out, int esp_pack, int cmvn, int grid_cap,
+                           int64_t clip_stride, float* out, int esp_pack, int cmvn, int grid_cap, float pre_emphasis,
                            hipStream_t stream) {
   const int nf = mode_b ? kNFramesB : (win_len - 320) / 256 + 1;
   const int n_chunks = mode_b ? 1 : (nf + kNFramesB - 1) / kNFramesB;
@@ -136,17 +136,17 @@ hipError_t launch_frontend(bool mode_b, bool i16, const void* audio, int64_t bat
   if (mode_b) {
     if (i16)
       hipLaunchKernelGGL((wk_frontend_kernel<true, int16_t>), dim3(grid), dim3(kFeBlock), 0, stream,
-                         (const int16_t*)audio, n_units, n_chunks, nf, win_len, clip_stride, out, esp_pack, cmvn);
+                         (const int16_t*)audio, n_units, n_chunks, nf, win_len, clip_stride, out, esp_pack, cmvn, -pre_emphasis);
     else
       hipLaunchKernelGGL((wk_frontend_kernel<true, float>), dim3(grid), dim3(kFeBlock), 0, stream,
-                         (const float*)audio, n_units, n_chunks, nf, win_len, clip_stride, out, esp_pack, cmvn);
+                         (const float*)audio, n_units, n_chunks, nf, win_len, clip_stride, out, esp_pack, cmvn, -pre_emphasis);
   } else {
     if (i16)
       hipLaunchKernelGGL((wk_frontend_kernel<false, int16_t>), dim3(grid), dim3(kFeBlock), 0, stream,
-                         (const int16_t*)audio, n_units, n_chunks, nf, win_len, clip_stride, out, esp_pack, cmvn);
+                         (const int16_t*)audio, n_units, n_chunks, nf, win_len, clip_stride, out, esp_pack, cmvn, -pre_emphasis);
     else
       hipLaunchKernelGGL((wk_frontend_kernel<false, float>), dim3(grid), dim3(kFeBlock), 0, stream,
-                         (const float*)audio, n_units, n_chunks, nf, win_len, clip_stride, out, esp_pack, cmvn);
+                         (const float*)audio, n_units, n_chunks, nf, win_len, clip_stride, out, esp_pack, cmvn, -pre_emphasis);
   }
   return hipGetLastError();
 }

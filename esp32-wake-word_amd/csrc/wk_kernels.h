@@ -31,7 +31,7 @@ wk_status on_device(int dev, F body) {
 // otherwise esp_mfcc -> [B][n_frames][13].
 hipError_t launch_frontend(bool mode_b, bool i16, const void* audio, int64_t batch, int win_len,
                            int64_t clip_stride, float* out, int esp_pack, int cmvn, int grid_cap,
-                           hipStream_t stream);
+                           float pre_emphasis, hipStream_t stream);   // pre_emphasis: 0.97 (mfcc.c:445), 0 = none
 
 // CNN (wk_cnn.hip): feats [B][13][63] -> logits [B].  `w` = device weight
 // blob in the packed WK_NUM_WEIGHTS layout of include/wakeword.h.

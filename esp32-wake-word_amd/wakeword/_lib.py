@@ -27,7 +27,7 @@ EXPORTS = ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_syn
            "wk_status_string", "wk_last_error", "wk_abi_version", "extract_mfcc", "free_mfcc",
            "analyze_mfcc_range", "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push",
            "wk_ctc_num_weights", "wk_ctc_create", "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward",
-           "wk_wav_read", "wk_wav_load_batch", "wk_augment")
+           "wk_wav_read", "wk_wav_load_batch", "wk_augment", "flow_extract_mfcc_single_frame")
 
 
 class WkConfig(C.Structure):
@@ -70,6 +70,8 @@ def _declare(L):
     L.extract_mfcc.restype = fp
     L.free_mfcc.argtypes = [fp]
     L.analyze_mfcc_range.argtypes = [fp, C.c_int, C.c_char_p]
+    L.flow_extract_mfcc_single_frame.argtypes = [fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.flow_extract_mfcc_single_frame.restype = fp
     L.wk_stream_create.argtypes = [vp, i32, i32, vp, C.POINTER(vp)]
     L.wk_stream_destroy.argtypes = [vp]
     L.wk_stream_reset.argtypes = [vp]

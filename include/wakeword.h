@@ -205,6 +205,10 @@ float* extract_mfcc(const float* signal, int signal_len, int sampling_rate, int 
                     int n_fft, int n_filters, int n_mfcc);
 void free_mfcc(float* mfcc);
 void analyze_mfcc_range(float* mfcc, int size, const char* label);
+/* mfcc.c:297-427 (defined there, not declared in mfcc.h): one 320-sample
+ * frame, no pre-emphasis -> malloc'd n_mfcc (<= 13) floats, NULL on error. */
+float* flow_extract_mfcc_single_frame(const float* frame, int frame_size, int sampling_rate, int n_fft, int n_filters,
+                                      int n_mfcc);
 
 #ifdef __cplusplus
 }

@@ -29,20 +29,23 @@ def lib():
         _lib.esp_mfcc_oracle.argtypes = [fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.c_int, fp]
         _lib.esp_mfcc_oracle.restype = C.c_int
+        _lib.esp_mfcc_oracle_ex.argtypes = [fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                            C.c_int, C.c_float, fp]
+        _lib.esp_mfcc_oracle_ex.restype = C.c_int
         _lib.esp_mfcc_oracle_fbank.argtypes = [C.c_int, C.c_int, C.c_int, fp]
         _lib.esp_mfcc_oracle_fbank.restype = C.c_int
     return _lib
 
 
 def esp_mfcc(x, esp_pack: bool = True, sr: int = 16000, frame: int = 320, hop: int = 256, n_fft: int = 512,
-             n_filters: int = 40, n_mfcc: int = 13) -> np.ndarray:
+             n_filters: int = 40, n_mfcc: int = 13, pre: float = 0.97) -> np.ndarray:
     """Mode-A MFCC of one signal -> (n_frames, n_mfcc) float32."""
     x = np.ascontiguousarray(x, np.float32)
     nf = (x.shape[0] - frame) // hop + 1
     out = np.zeros((max(nf, 1), n_mfcc), np.float32)
     fp = C.POINTER(C.c_float)
-    rc = lib().esp_mfcc_oracle(x.ctypes.data_as(fp), x.shape[0], sr, frame, hop, n_fft, n_filters, n_mfcc,
-                               int(esp_pack), out.ctypes.data_as(fp))
+    rc = lib().esp_mfcc_oracle_ex(x.ctypes.data_as(fp), x.shape[0], sr, frame, hop, n_fft, n_filters, n_mfcc,
+                                  int(esp_pack), pre, out.ctypes.data_as(fp))
     if rc < 0:
         raise ValueError("esp_mfcc_oracle rejected the arguments")
     return out[:rc]

@@ -74,9 +74,11 @@ int esp_mfcc_oracle_fbank(int sr, int n_filters, int n_fft, float* fb) {
 }
 
 /* Mode-A MFCC of one signal -> out[n_frames][n_mfcc] (frame-major).
- * Returns n_frames, or -1 on bad arguments / allocation failure. */
-int esp_mfcc_oracle(const float* x, int L, int sr, int frame, int hop, int n_fft, int n_filters, int n_mfcc,
-                    int esp_pack, float* out) {
+ * Returns n_frames, or -1 on bad arguments / allocation failure.  `pre` is the
+ * pre-emphasis coefficient: 0.97 for extract_mfcc (mfcc.c:445), 0 for
+ * flow_extract_mfcc_single_frame (mfcc.c:297-427, which has none). */
+int esp_mfcc_oracle_ex(const float* x, int L, int sr, int frame, int hop, int n_fft, int n_filters, int n_mfcc,
+                       int esp_pack, float pre, float* out) {
   if (!x || !out || L < frame || frame <= 0 || hop <= 0 || n_fft < frame || n_filters <= 0 || n_mfcc <= 0 ||
       n_mfcc > n_filters)
     return -1;
@@ -96,7 +98,7 @@ int esp_mfcc_oracle(const float* x, int L, int sr, int frame, int hop, int n_fft
     goto done;
   }
   y[0] = x[0];
-  for (int i = 1; i < L; ++i) y[i] = x[i] - 0.97f * x[i - 1];
+  for (int i = 1; i < L; ++i) y[i] = x[i] - pre * x[i - 1];
   for (int i = 0; i < frame; ++i) win[i] = 0.53836f - (1.0f - 0.53836f) * cosf(2.0f * M_PI * i / (frame - 1));
   for (int i = 0; i < n_fft; ++i) {
     cs[i] = cos(2.0 * M_PI * i / n_fft);
@@ -134,4 +136,9 @@ int esp_mfcc_oracle(const float* x, int L, int sr, int frame, int hop, int n_fft
 done:
   free(y); free(win); free(fb); free(pw); free(mel); free(ct); free(cs); free(sn); free(fr);
   return rc;
+}
+
+int esp_mfcc_oracle(const float* x, int L, int sr, int frame, int hop, int n_fft, int n_filters, int n_mfcc,
+                    int esp_pack, float* out) {
+  return esp_mfcc_oracle_ex(x, L, sr, frame, hop, n_fft, n_filters, n_mfcc, esp_pack, 0.97f, out);
 }

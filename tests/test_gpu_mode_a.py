@@ -65,3 +65,24 @@ def test_extract_mfcc_shim_matches_oracle(gpu):
     assert wakeword.extract_mfcc(x[:100], 100) is None
     # Parameters outside the reference configuration are refused (NULL), not approximated.
     assert wakeword.extract_mfcc(x, 16192, 16000, 400, 160, 512, 40, 13) is None
+
+
+def test_single_frame_shim_matches_oracle(gpu):
+    """mfcc.c:297-427 flow_extract_mfcc_single_frame: no pre-emphasis, one frame."""
+    import ctypes as C
+    from wakeword import _lib
+    L = _lib.lib()
+    fp = C.POINTER(C.c_float)
+    for seed in (1, 2, 3):
+        frame = O.synth_clips(seed, 0, 1, 320)[0]
+        p = L.flow_extract_mfcc_single_frame(frame.ctypes.data_as(fp), 320, 16000, 512, 40, 13)
+        assert p
+        got = np.ctypeslib.as_array(p, shape=(13,)).copy()
+        L.free_mfcc(p)
+        ref = B.esp_mfcc(frame, pre=0.0)[0]
+        assert np.abs(got - ref).max() <= _tol(ref)
+        p5 = L.flow_extract_mfcc_single_frame(frame.ctypes.data_as(fp), 320, 16000, 512, 40, 5)
+        np.testing.assert_array_equal(np.ctypeslib.as_array(p5, shape=(5,)), got[:5])
+        L.free_mfcc(p5)
+    assert not L.flow_extract_mfcc_single_frame(None, 320, 16000, 512, 40, 13)            # mfcc.c:300-303
+    assert not L.flow_extract_mfcc_single_frame(frame.ctypes.data_as(fp), 600, 16000, 512, 40, 13)
