@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                    help="CNN convolutions: fp32 (config 2, default) or bf16 (config 4); front-end fp32 either way")
     return ap.parse_args()
 
 
@@ -106,7 +108,8 @@ def main():
             dist.barrier()
 
     B = args.batch
-    model = wakeword.load_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"), device=local)
+    model = wakeword.load_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"), device=local,
+                               precision=args.precision)
     first, count = weak_shard(B, rank)                     # per-rank clip split, no collective
     clips = wakeword.synth_clips(args.seed, first, count, 16000, device=local)   # resident in HBM
     logits = torch.empty((B,), dtype=torch.float32, device=f"cuda:{local}")
@@ -160,10 +163,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if args.precision == "fp32" else "bf16 convolutions, f32 front-end/classifier",
             "data": "synthetic: device counter-hash generator, clamp(0.1*N(0,1))+440 Hz sine on odd clips "
                     "(SURVEY 8(d) config 2); xiaoa.onnx weights",
-            "config": {"workload": "config2: fused MFCC(torchaudio+CMVN)+xiaoa CNN fp32, B clips per GPU",
+            "config": {"workload": ("config2: fused MFCC(torchaudio+CMVN)+xiaoa CNN fp32, B clips per GPU"
+                                    if args.precision == "fp32" else
+                                    "config4: fused MFCC(torchaudio+CMVN) fp32 + xiaoa CNN bf16, B clips per GPU"),
                        "batch_per_gpu": B, "global_batch": world * B, "seq_len": 16000,
                        "parallelism": f"dp{world} (per-rank clip split, no collectives)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,

@@ -18,6 +18,7 @@ struct wk_handle {
   float* d_packed;       // fragment-major weights (wk::pack_fragments) for the fused kernel
   float* d_feats_ws;     // feature workspace for the unfused path
   int8_t* d_int8;        // int8 weights (WK_PREC_INT8, wk::quantize_int8_weights)
+  uint16_t* d_bf16;      // bf16 conv fragments (WK_PREC_BF16, wk::pack_fragments_bf16)
   int64_t ws_clips;
   int unfused;           // WAKEWORD_UNFUSED=1: front-end + CNN as two kernels (A/B testing)
   int fused_exp;         // WAKEWORD_FUSED_EXP: role-isolation timing experiments (wrong logits)
@@ -109,6 +110,13 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
       if ((e2 = hipMemcpy(h->d_packed, pk.data(), sizeof(float) * wk::kNumPacked, hipMemcpyHostToDevice)) !=
           hipSuccess)
         return hip_fail(e2, "hipMemcpy(packed weights)");
+      if (cfg->precision == WK_PREC_BF16) {
+        std::vector<uint16_t> pb(wk::kNumPackedBf16);
+        wk::pack_fragments_bf16(host_weights, pb.data());
+        if ((e2 = hipMalloc(&h->d_bf16, pb.size() * 2)) != hipSuccess) return hip_fail(e2, "hipMalloc(bf16 weights)");
+        if ((e2 = hipMemcpy(h->d_bf16, pb.data(), pb.size() * 2, hipMemcpyHostToDevice)) != hipSuccess)
+          return hip_fail(e2, "hipMemcpy(bf16 weights)");
+      }
       if (cfg->precision == WK_PREC_INT8) {
         std::vector<int8_t> q(wk::kNumInt8Weights);
         wk::quantize_int8_weights(host_weights, q.data());
@@ -137,6 +145,7 @@ wk_status wk_destroy(wk_handle* h) {
     if (h->d_feats_ws) (void)hipFree(h->d_feats_ws);
     if (h->d_packed) (void)hipFree(h->d_packed);
     if (h->d_int8) (void)hipFree(h->d_int8);
+    if (h->d_bf16) (void)hipFree(h->d_bf16);
     return WK_OK;
   });
   free(h);
@@ -174,7 +183,7 @@ wk_status wk_cnn(wk_handle* h, const float* d_feats, int64_t batch, float* d_log
   if (!h->d_weights) return invalid("wk_cnn: handle created without weights");
   if (batch < 0 || (batch > 0 && (!d_feats || !d_logits))) return invalid("wk_cnn: bad arguments");
   if (h->cfg.precision == WK_PREC_BF16) {
-    g_last_error = "bf16 CNN not implemented in this build";
+    g_last_error = "wk_cnn: bf16 convolutions run inside the fused kernel only (use wk_forward)";
     return WK_ERR_UNSUPPORTED;
   }
   return on_device(h->cfg.device, [&]() -> wk_status {
@@ -196,15 +205,11 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
   wk_status s = check_audio(d_audio, dtype, batch, win_len, clip_stride, true);
   if (s != WK_OK) return s;
   if (batch > 0 && !d_logits) return invalid("wk_forward: null logits");
-  if (h->cfg.precision == WK_PREC_BF16) {
-    g_last_error = "bf16 CNN not implemented in this build";
-    return WK_ERR_UNSUPPORTED;
-  }
   const bool int8 = h->cfg.precision == WK_PREC_INT8;
   return on_device(h->cfg.device, [&]() -> wk_status {
-    if (!h->unfused && !int8) {
-      hipError_t e = wk::launch_fused(dtype == WK_DTYPE_I16, d_audio, batch, clip_stride, h->d_packed, d_logits,
-                                      d_feats_or_null, h->n_cu, (hipStream_t)stream, h->fused_exp);
+    if ((!h->unfused && !int8) || h->d_bf16) {   // bf16 convolutions exist only in the fused kernel
+      hipError_t e = wk::launch_fused(dtype == WK_DTYPE_I16, d_audio, batch, clip_stride, h->d_packed, h->d_bf16,
+                                      d_logits, d_feats_or_null, h->n_cu, (hipStream_t)stream, h->fused_exp);
       return e == hipSuccess ? WK_OK : hip_fail(e, "fused launch");
     }
     const size_t esz = dtype == WK_DTYPE_I16 ? 2 : 4;

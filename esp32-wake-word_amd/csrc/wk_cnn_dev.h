@@ -65,4 +65,54 @@ __device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g,
   }
 }
 
+// ---- bf16 convolutions (v_mfma_f32_16x16x16_bf16; WK_PREC_BF16) ----------
+typedef short s4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma_bf16(s4 a, s4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t bf16_bits(float x) {   // round to nearest even
+  const uint32_t u = __float_as_uint(x);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+// Two 16-column t-tiles of one conv layer from a bf16 [clip][t][ci] image
+// (ci pitch CIP).  Step s covers k = 16s..16s+15 = (tap = s / CB, ci block
+// s % CB); boff = this lane's element offset (t row + 4 (lane >> 4)).
+template <int NSTEP, int CB, int CIP, int CHUNK = 0>
+__device__ __forceinline__ void conv_pair_bf(const uint16_t* __restrict__ img, const s4 (&wf)[NSTEP], int boff_a,
+                                             int boff_b, f32x4& acc_a, f32x4& acc_b) {
+#pragma unroll
+  for (int s = 0; s < NSTEP; ++s) {
+    const int off = (s / CB) * CIP + 16 * (s % CB);
+    const s4 ba = *reinterpret_cast<const s4*>(img + boff_a + off);
+    const s4 bb = *reinterpret_cast<const s4*>(img + boff_b + off);
+    acc_a = mfma_bf16(wf[s], ba, acc_a);
+    acc_b = mfma_bf16(wf[s], bb, acc_b);
+    if (CHUNK > 0 && (s % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ReLU -> maxpool(2) -> the 4 pooled channels of this lane (consecutive co)
+// as one 8-byte store into the next layer's bf16 [clip][t][ci] image.
+template <int CIP_N, int TP_N, int TN>
+__device__ __forceinline__ void epi_pool_bf(const f32x4& acc, uint16_t* __restrict__ next, int co0, int clip, int t0,
+                                            int lane) {
+  const int t = t0 + (lane & 15);
+  const int tp = t >> 1;
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float x = fmaxf(acc[r], 0.0f);
+    v[r] = fmaxf(x, swap_adjacent(x));
+  }
+  if (!(lane & 1) && tp < TN) {
+    uint2 pkd;
+    pkd.x = bf16_bits(v[0]) | (bf16_bits(v[1]) << 16);
+    pkd.y = bf16_bits(v[2]) | (bf16_bits(v[3]) << 16);
+    *reinterpret_cast<uint2*>(next + (clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4)) = pkd;
+  }
+}
+
 }  // namespace wk

@@ -41,19 +41,34 @@ __device__ unsigned long long g_wk_stamps[16][16];
 
 constexpr int NBF = 4;               // clips per CNN batch
 constexpr int kFusedBlock = 1024;    // 8 front-end + 8 CNN waves
-// CNN images (floats); ci pitches are 16 mod 32 (conflict-free B fragments).
+// LDS carve after the front-end's (wk_fe_dev.h): fixed tail, then the CNN
+// images -- fp32 [ci][clip][t] images, or (bf16 convolutions) bf16
+// [clip][t][ci] images, overlaying the same region.
+constexpr int kGOff = kFeLds;                       // pooled features [128][4]
+constexpr int kFcpOff = kGOff + 128 * NBF;          // classifier.0 partials [2][64][4]
+constexpr int kL1Off = kFcpOff + 2 * 64 * NBF;      // second log-mel buffer [40][64] (first: kLOff)
+constexpr int kCtrlOff = kL1Off + kLSize;           // control words
+constexpr int kImgOff = (kCtrlOff + 16 + 3) & ~3;   // 16-byte aligned
+static_assert(kImgOff % 2 == 0, "8-byte aligned bf16 images");
+// fp32 images; ci pitches are 16 mod 32 (conflict-free B fragments).
 constexpr int F0_CLIP = 66, F0_CI = NBF * 66 + 8;   // conv1 input [16 ci][4][66], pitch 272
 constexpr int F1_CLIP = 34, F1_CI = NBF * 34 + 8;   // conv2 input [32 ci][4][34], pitch 144
 constexpr int F2_CLIP = 18, F2_CI = NBF * 18 + 8;   // conv3 input [64 ci][4][18], pitch 80
 static_assert(F0_CI % 32 == 16 && F1_CI % 32 == 16 && F2_CI % 32 == 16, "bank-conflict-free pitches");
-constexpr int kF0Off = kFeLds;
+constexpr int kF0Off = kImgOff;
 constexpr int kF1Off = kF0Off + 16 * F0_CI;
 constexpr int kF2Off = kF1Off + 32 * F1_CI;
-constexpr int kGOff = kF2Off + 64 * F2_CI;          // pooled features [128][4]
-constexpr int kFcpOff = kGOff + 128 * NBF;          // classifier.0 partials [2][64][4]
-constexpr int kL1Off = kFcpOff + 2 * 64 * NBF;      // second log-mel buffer [40][64] (first: kLOff)
-constexpr int kCtrlOff = kL1Off + kLSize;           // control words
-constexpr int kFusedLds = kCtrlOff + 16;
+constexpr int kImgEnd = kF2Off + 64 * F2_CI;
+// bf16 images [clip][t][ci], ci pitch = Cin + 4 (t stride of 10 / 18 / 34
+// dwords: the 16 t-lanes of a B-fragment read hit distinct bank pairs).
+constexpr int B0_CIP = 20, B1_CIP = 36, B2_CIP = 68;                 // uint16 units
+constexpr int B0_TP = 66, B1_TP = 34, B2_TP = 18;                    // t positions incl. guards
+constexpr int kB0Off = kImgOff;                                      // float units
+constexpr int kB1Off = kB0Off + NBF * B0_TP * B0_CIP / 2;
+constexpr int kB2Off = kB1Off + NBF * B1_TP * B1_CIP / 2;
+static_assert(kB2Off + NBF * B2_TP * B2_CIP / 2 <= kImgEnd, "bf16 images overlay the fp32 region");
+static_assert((kB1Off % 2) == 0 && (kB2Off % 2) == 0, "8-byte aligned bf16 images");
+constexpr int kFusedLds = kImgEnd;
 static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 
 enum { kCtrlFeBar = 0, kCtrlCnnBar = 1, kCtrlLReady = 2, kCtrlLFree = 3, kCtrlAbort = 15 };
@@ -174,14 +189,22 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
 // ---------------------------------------------------------------------------
 // CNN role (waves 8-15): batches of NBF clips from the conv1 image.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ pk, int64_t n_mine,
-                                         float* __restrict__ logits, float* __restrict__ feats_out, int cw, int lane,
-                                         int exp_flags) {
+template <bool BF>
+__device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ pk, const uint16_t* __restrict__ pkb,
+                                         int64_t n_mine, float* __restrict__ logits, float* __restrict__ feats_out,
+                                         int cw, int lane, int exp_flags) {
   const float* L = smem + kLOff;
   const float* L1 = smem + kL1Off;
   float* F0 = smem + kF0Off;
   float* F1 = smem + kF1Off;
   float* F2 = smem + kF2Off;
+  uint16_t* B0 = reinterpret_cast<uint16_t*>(smem + kB0Off);
+  uint16_t* B1 = reinterpret_cast<uint16_t*>(smem + kB1Off);
+  uint16_t* B2 = reinterpret_cast<uint16_t*>(smem + kB2Off);
+  const auto rsb = make_rsrc(pkb, 2 * kNumPackedBf16);
+  auto frag_bf = [&](int elem_off) -> s4 {   // one lane's 4 bf16 of the fragment at elem_off (x 64 lanes x 4)
+    return __builtin_bit_cast(s4, __builtin_amdgcn_raw_buffer_load_b64(rsb, 8 * lane, 2 * elem_off, 0));
+  };
   float* Gp = smem + kGOff;
   float* FCP = smem + kFcpOff;
   unsigned* ctrl = reinterpret_cast<unsigned*>(smem + kCtrlOff);
@@ -195,7 +218,11 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   // 256-byte load per A fragment.  conv3's (48 fragments) stay in VGPRs; the
   // other layers' are re-read from L2 per batch.
   float w3[48];
-  {
+  s4 w3b[12];
+  if constexpr (BF) {
+#pragma unroll
+    for (int s = 0; s < 12; ++s) w3b[s] = frag_bf(kPbW3 + (cw * 12 + s) * 256);
+  } else {
 #pragma unroll
     for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
   }
@@ -203,7 +230,11 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   WK_STAMP_INIT
   for (int64_t b = 0; b < n_batches; ++b) {
     float w1[12];
-    {
+    s4 w1b[3];
+    if constexpr (BF) {
+#pragma unroll
+      for (int s = 0; s < 3; ++s) w1b[s] = frag_bf(kPbW1 + ((cw & 1) * 3 + s) * 256);
+    } else {
 #pragma unroll
       for (int s = 0; s < 12; ++s) w1[s] = buf_load(rs, lv, 4 * (kPkW1 + ((cw & 1) * 12 + s) * 64));
     }
@@ -222,14 +253,19 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         const float* lrow = (i & 1 ? L1 : L) + ln;
         const int k = (cw + 3 * s) & 7;
         float* f0 = F0 + s * F0_CLIP + 1 + ln;
+        uint16_t* f0b = B0 + (s * B0_TP + 1 + ln) * B0_CIP;
         float* fo = feats_out ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) + ln : nullptr;
         if (k < 5) {
           const int c0 = 2 * k;
           float y0 = dct_coef<true>(c0, lrow), y1 = dct_coef<true>(c0 + 1, lrow);
           cmvn_lane2(y0, y1, valid, kNFramesB);
-          if (valid) {
+          if (valid && BF) {
+            *reinterpret_cast<uint32_t*>(f0b + c0) = bf16_bits(y0) | (bf16_bits(y1) << 16);   // c0 even
+          } else if (valid) {
             f0[c0 * F0_CI] = y0;
             f0[(c0 + 1) * F0_CI] = y1;
+          }
+          if (valid) {
             if (fo) {
               fo[c0 * kNFramesB] = y0;
               fo[(c0 + 1) * kNFramesB] = y1;
@@ -239,7 +275,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
           const int c0 = k + 5;
           const float y = cmvn_lane(dct_coef<true>(c0, lrow), valid, kNFramesB);
           if (valid) {
-            f0[c0 * F0_CI] = y;
+            if (BF) f0b[c0] = (uint16_t)bf16_bits(y); else f0[c0 * F0_CI] = y;
             if (fo) fo[c0 * kNFramesB] = y;
           }
         }
@@ -257,9 +293,16 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
       for (int p = 0; p < 2; ++p) {
         const int ta = 32 * p, tb = ta + 16;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
-        conv_pair<12, F0_CI, 4, 6>(F0, w1, bo + ta, bo + tb, acc_a, acc_b);
-        epi_pool<F1_CI, F1_CLIP, 31>(acc_a, F1, co0, cl, ta, lane);
-        epi_pool<F1_CI, F1_CLIP, 31>(acc_b, F1, co0, cl, tb, lane);
+        if constexpr (BF) {
+          const int bb = (cl * B0_TP + li) * B0_CIP + 4 * lk;
+          conv_pair_bf<3, 1, B0_CIP>(B0, w1b, bb + ta * B0_CIP, bb + tb * B0_CIP, acc_a, acc_b);
+          epi_pool_bf<B1_CIP, B1_TP, 31>(acc_a, B1, co0, cl, ta, lane);
+          epi_pool_bf<B1_CIP, B1_TP, 31>(acc_b, B1, co0, cl, tb, lane);
+        } else {
+          conv_pair<12, F0_CI, 4, 6>(F0, w1, bo + ta, bo + tb, acc_a, acc_b);
+          epi_pool<F1_CI, F1_CLIP, 31>(acc_a, F1, co0, cl, ta, lane);
+          epi_pool<F1_CI, F1_CLIP, 31>(acc_b, F1, co0, cl, tb, lane);
+        }
       }
     }
     WK_STAMP(1);
@@ -267,7 +310,21 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     WK_STAMP(2);
 
     // conv2: co tile (cw&3), clips 2*(cw>>2) + {0,1}, 2 t-tiles each.
-    {
+    if constexpr (BF) {
+      s4 w2b[6];
+#pragma unroll
+      for (int s = 0; s < 6; ++s) w2b[s] = frag_bf(kPbW2 + ((cw & 3) * 6 + s) * 256);
+      const int co0 = 16 * (cw & 3);
+#pragma unroll 1
+      for (int p = 0; p < 2; ++p) {
+        const int cl = 2 * (cw >> 2) + p;
+        const int bb = (cl * B1_TP + li) * B1_CIP + 4 * lk;
+        f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
+        conv_pair_bf<6, 2, B1_CIP>(B1, w2b, bb, bb + 16 * B1_CIP, acc_a, acc_b);
+        epi_pool_bf<B2_CIP, B2_TP, 15>(acc_a, B2, co0, cl, 0, lane);
+        epi_pool_bf<B2_CIP, B2_TP, 15>(acc_b, B2, co0, cl, 16, lane);
+      }
+    } else {
       float w2[24];
 #pragma unroll
       for (int s = 0; s < 24; ++s) w2[s] = buf_load(rs, lv, 4 * (kPkW2 + ((cw & 3) * 24 + s) * 64));
@@ -294,7 +351,12 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
       for (int p = 0; p < 2; ++p) {
         const int ca = 2 * p, cb = 2 * p + 1;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
-        conv_pair<48, F2_CI, 16, 8>(F2, w3, bo + ca * F2_CLIP, bo + cb * F2_CLIP, acc_a, acc_b);
+        if constexpr (BF) {
+          const int bb = li * B2_CIP + 4 * lk;
+          conv_pair_bf<12, 4, B2_CIP, 6>(B2, w3b, bb + ca * B2_TP * B2_CIP, bb + cb * B2_TP * B2_CIP, acc_a, acc_b);
+        } else {
+          conv_pair<48, F2_CI, 16, 8>(F2, w3, bo + ca * F2_CLIP, bo + cb * F2_CLIP, acc_a, acc_b);
+        }
         epi_gap<NBF>(acc_a, Gp, co0, ca, lane);
         epi_gap<NBF>(acc_b, Gp, co0, cb, lane);
       }
@@ -349,9 +411,10 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   WK_STAMP_FLUSH(8 + cw);
 }
 
-template <typename T>
+template <typename T, bool BF>
 __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __restrict__ audio, int64_t batch,
                                                                  int64_t clip_stride, const float* __restrict__ wts,
+                                                                 const uint16_t* __restrict__ wbf,
                                                                  float* __restrict__ logits,
                                                                  float* __restrict__ feats_out, int exp_flags) {
   __shared__ __attribute__((aligned(16))) float smem[kFusedLds];
@@ -359,7 +422,7 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   fe_init_tables<true>(smem, tid, kFusedBlock);
-  for (int i = tid; i < kFusedLds - kF0Off; i += kFusedBlock) smem[kF0Off + i] = 0.0f;  // guards, pads, ctrl
+  for (int i = tid; i < kFusedLds - kGOff; i += kFusedBlock) smem[kGOff + i] = 0.0f;  // ctrl, guards, pads
   __syncthreads();
   const int64_t n_mine = batch > (int64_t)blockIdx.x ? (batch - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   if (wave < 8) {
@@ -368,7 +431,7 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
 #endif
   } else {
 #ifndef WK_EXPERIMENT_NO_CNN
-    if (!(exp_flags & 1)) cnn_role(smem, wts, n_mine, logits, feats_out, wave - 8, lane, exp_flags);
+    if (!(exp_flags & 1)) cnn_role<BF>(smem, wts, wbf, n_mine, logits, feats_out, wave - 8, lane, exp_flags);
 #endif
   }
 }
@@ -389,15 +452,23 @@ extern "C" int wk_debug_stamps(unsigned long long* host_out, int reset) {
 namespace wk {
 
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
-                        float* logits, float* feats_or_null, int grid_cap, hipStream_t stream, int exp_flags) {
+                        const uint16_t* wbf, float* logits, float* feats_or_null, int grid_cap, hipStream_t stream,
+                        int exp_flags) {
   if (batch == 0) return hipSuccess;
   const int grid = (int)(batch < grid_cap ? batch : grid_cap);
-  if (i16)
-    hipLaunchKernelGGL(wk_fused_kernel<int16_t>, dim3(grid), dim3(kFusedBlock), 0, stream, (const int16_t*)audio,
-                       batch, clip_stride, w, logits, feats_or_null, exp_flags);
+  const dim3 g(grid), blk(kFusedBlock);
+  if (i16 && wbf)
+    hipLaunchKernelGGL((wk_fused_kernel<int16_t, true>), g, blk, 0, stream, (const int16_t*)audio, batch, clip_stride,
+                       w, wbf, logits, feats_or_null, exp_flags);
+  else if (i16)
+    hipLaunchKernelGGL((wk_fused_kernel<int16_t, false>), g, blk, 0, stream, (const int16_t*)audio, batch, clip_stride,
+                       w, wbf, logits, feats_or_null, exp_flags);
+  else if (wbf)
+    hipLaunchKernelGGL((wk_fused_kernel<float, true>), g, blk, 0, stream, (const float*)audio, batch, clip_stride, w,
+                       wbf, logits, feats_or_null, exp_flags);
   else
-    hipLaunchKernelGGL(wk_fused_kernel<float>, dim3(grid), dim3(kFusedBlock), 0, stream, (const float*)audio, batch,
-                       clip_stride, w, logits, feats_or_null, exp_flags);
+    hipLaunchKernelGGL((wk_fused_kernel<float, false>), g, blk, 0, stream, (const float*)audio, batch, clip_stride, w,
+                       wbf, logits, feats_or_null, exp_flags);
   return hipGetLastError();
 }
 

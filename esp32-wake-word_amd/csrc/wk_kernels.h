@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string.h>
+
 #include <string>
 
 #include "wakeword.h"
@@ -39,8 +41,10 @@ hipError_t launch_cnn(const float* feats, int64_t batch, const float* w, float* 
                       int grid_cap, hipStream_t stream);
 
 // Fused front-end + CNN (wk_fused.hip), mode B only.
+// w = fp32 fragment-major weights (pack_fragments); wbf = bf16 conv fragments
+// (pack_fragments_bf16) or null: non-null selects bf16 convolutions (config 4).
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
-                        float* logits, float* feats_or_null, int grid_cap, hipStream_t stream,
+                        const uint16_t* wbf, float* logits, float* feats_or_null, int grid_cap, hipStream_t stream,
                         int exp_flags = 0);   // exp_flags (timing experiments only): 1 = FE role only, 2 = CNN only
 
 // int8 CNN in the device's esp-dl arithmetic (wk_int8.hip); feats [B][13][63] fp32.
@@ -73,6 +77,39 @@ constexpr int kPkW3 = kPkW2 + 4 * 24 * 64;      // [8][48][64]
 constexpr int kPkF1 = kPkW3 + 8 * 48 * 64;      // [4 o-tiles][32 s][64]  (k = 4s + lane>>4)
 constexpr int kPkF2 = kPkF1 + 4 * 32 * 64;      // [64]
 constexpr int kNumPacked = kPkF2 + 64;
+
+// bf16 variant (WK_PREC_BF16, v_mfma_f32_16x16x16_bf16): per 16-row tile and
+// k-step s (k = 16s..16s+15), lane l feeds 4 consecutive k = 16s + 4(l>>4) + j
+// (j = 0..3) of row l&15 -- one 8-byte load per fragment.  k = tap*Cin_pad + ci.
+// Offsets in bf16 (uint16) units.
+constexpr int kPbW1 = 0;                        // [2 tiles][3 s][64][4]   (Cin 13 padded to 16)
+constexpr int kPbW2 = kPbW1 + 2 * 3 * 64 * 4;   // [4][6][64][4]
+constexpr int kPbW3 = kPbW2 + 4 * 6 * 64 * 4;   // [8][12][64][4]
+constexpr int kNumPackedBf16 = kPbW3 + 8 * 12 * 64 * 4;
+
+inline uint16_t to_bf16_rne(float x) {
+  uint32_t u;
+  memcpy(&u, &x, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+inline void pack_fragments_bf16(const float* w, uint16_t* pk) {
+  auto pack = [&](int off, int cout_tiles, int cin, int cin_pad, int wbase) {
+    const int nsteps = 3 * cin_pad / 16;
+    for (int t = 0; t < cout_tiles; ++t)
+      for (int s = 0; s < nsteps; ++s)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 4; ++j) {
+            const int co = 16 * t + (l & 15), k = 16 * s + 4 * (l >> 4) + j, tap = k / cin_pad, ci = k % cin_pad;
+            pk[off + ((t * nsteps + s) * 64 + l) * 4 + j] =
+                ci < cin ? to_bf16_rne(w[wbase + (co * cin + ci) * 3 + tap]) : (uint16_t)0;
+          }
+  };
+  pack(kPbW1, 2, 13, 16, kOffW1);
+  pack(kPbW2, 4, 32, 32, kOffW2);
+  pack(kPbW3, 8, 64, 64, kOffW3);
+}
 
 // Host-side packing of the WK_NUM_WEIGHTS blob into the fragment-major layout.
 inline void pack_fragments(const float* w, float* pk) {

@@ -1,0 +1,44 @@
+"""bf16 mode (WK_PREC_BF16): bf16 convolutions
+(v_mfma_f32_16x16x16_bf16, fp32 accumulation) inside the fused kernel, fp32
+front-end and classifier.  Tolerance vs the fp32 reference path: 0.05 in logit
+(bf16 keeps 8 mantissa bits; observed ~1e-2), identical decisions on the
+reference WAVs."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import wk_oracle as O
+
+pytestmark = pytest.mark.gpu
+BF16_LOGIT_ATOL = 0.05
+
+
+@pytest.fixture(scope="module")
+def m16(gpu, golden_dir):
+    import wakeword
+    return wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"), precision="bf16")
+
+
+def test_bf16_golden_wavs(m16, golden_dir):
+    w = np.load(os.path.join(golden_dir, "wavs.npz"))
+    got = m16.detect(w["x_noise"]).reshape(-1).cpu().numpy()
+    ref = w["logit_noise"].reshape(-1)
+    assert np.abs(got - ref).max() <= BF16_LOGIT_ATOL
+    assert ((got > 0) == (ref > 0)).all()
+
+
+@pytest.mark.parametrize("n", [1, 5, 300])
+def test_bf16_synth_vs_oracle_and_batch_invariance(m16, xiaoa_sd, n):
+    x = O.synth_clips(31, 0, n, 16000)
+    got = m16.detect(x).reshape(-1).cpu().numpy()
+    ref = O.detect_mode_b(x[: min(n, 32)].astype(np.float64), xiaoa_sd)
+    assert np.abs(got[: ref.size] - ref).max() <= BF16_LOGIT_ATOL
+    one = m16.detect(x[:1]).reshape(-1).cpu().numpy()
+    np.testing.assert_array_equal(one, got[:1])      # per-clip results do not depend on the batch
+
+
+def test_bf16_cnn_only_entry_is_refused(m16):
+    import wakeword
+    with pytest.raises(wakeword.WakewordError, match="UNSUPPORTED"):
+        m16(np.zeros((2, 13, 63), np.float32))
