@@ -115,4 +115,48 @@ __device__ __forceinline__ void epi_pool_bf(const f32x4& acc, uint16_t* __restri
   }
 }
 
+// ---- fp32 convolutions from [clip][t][ci] images (ci-blocked K order) ----
+// MFMA K order is free as long as A and B agree: lane group q = lane >> 4
+// takes ci = 16 cb + 4 q + j at step (tap, cb, j), so the B values of 4
+// consecutive steps are 4 consecutive ci at one (t + tap) row -- one
+// ds_read_b128 per 4 v_mfma_f32_16x16x4f32 (A packed to match,
+// wk_kernels.h pack_fragments).  NSTEP = 3 taps * CB ci-blocks * 4.
+template <int CB, int CIP, int CHUNK = 0>
+__device__ __forceinline__ void conv_pair_v(const float* __restrict__ img, const float (&wf)[12 * CB], int boff_a,
+                                            int boff_b, f32x4& acc_a, f32x4& acc_b) {
+#pragma unroll
+  for (int g = 0; g < 3 * CB; ++g) {   // g = tap * CB + cb
+    const int off = (g / CB) * CIP + 16 * (g % CB);
+    const float4 ba = *reinterpret_cast<const float4*>(img + boff_a + off);
+    const float4 bb = *reinterpret_cast<const float4*>(img + boff_b + off);
+    acc_a = mfma4(wf[4 * g + 0], ba.x, acc_a);
+    acc_b = mfma4(wf[4 * g + 0], bb.x, acc_b);
+    acc_a = mfma4(wf[4 * g + 1], ba.y, acc_a);
+    acc_b = mfma4(wf[4 * g + 1], bb.y, acc_b);
+    acc_a = mfma4(wf[4 * g + 2], ba.z, acc_a);
+    acc_b = mfma4(wf[4 * g + 2], bb.z, acc_b);
+    acc_a = mfma4(wf[4 * g + 3], ba.w, acc_a);
+    acc_b = mfma4(wf[4 * g + 3], bb.w, acc_b);
+    if (CHUNK > 0 && (g % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ReLU -> maxpool(2) -> this lane's 4 pooled channels (consecutive co) as one
+// 16-byte store into the next layer's fp32 [clip][t][ci] image.
+template <int CIP_N, int TP_N, int TN>
+__device__ __forceinline__ void epi_pool_v(const f32x4& acc, float* __restrict__ next, int co0, int clip, int t0,
+                                           int lane) {
+  const int t = t0 + (lane & 15);
+  const int tp = t >> 1;
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float x = fmaxf(acc[r], 0.0f);
+    v[r] = fmaxf(x, swap_adjacent(x));
+  }
+  if (!(lane & 1) && tp < TN)
+    *reinterpret_cast<float4*>(next + (clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4)) =
+        make_float4(v[0], v[1], v[2], v[3]);
+}
+
 }  // namespace wk

@@ -42,32 +42,26 @@ __device__ unsigned long long g_wk_stamps[16][16];
 constexpr int NBF = 4;               // clips per CNN batch
 constexpr int kFusedBlock = 1024;    // 8 front-end + 8 CNN waves
 // LDS carve after the front-end's (wk_fe_dev.h): fixed tail, then the CNN
-// images -- fp32 [ci][clip][t] images, or (bf16 convolutions) bf16
-// [clip][t][ci] images, overlaying the same region.
+// images [clip][t][ci] -- fp32, or bf16 for bf16 convolutions -- overlaying
+// one region.  ci pitch = Cin + 4 elements: the 16 t-lanes of a B-fragment
+// read (16 B fp32 / 8 B bf16 per lane) land on distinct bank groups.
 constexpr int kGOff = kFeLds;                       // pooled features [128][4]
 constexpr int kFcpOff = kGOff + 128 * NBF;          // classifier.0 partials [2][64][4]
 constexpr int kL1Off = kFcpOff + 2 * 64 * NBF;      // second log-mel buffer [40][64] (first: kLOff)
 constexpr int kCtrlOff = kL1Off + kLSize;           // control words
 constexpr int kImgOff = (kCtrlOff + 16 + 3) & ~3;   // 16-byte aligned
-static_assert(kImgOff % 2 == 0, "8-byte aligned bf16 images");
-// fp32 images; ci pitches are 16 mod 32 (conflict-free B fragments).
-constexpr int F0_CLIP = 66, F0_CI = NBF * 66 + 8;   // conv1 input [16 ci][4][66], pitch 272
-constexpr int F1_CLIP = 34, F1_CI = NBF * 34 + 8;   // conv2 input [32 ci][4][34], pitch 144
-constexpr int F2_CLIP = 18, F2_CI = NBF * 18 + 8;   // conv3 input [64 ci][4][18], pitch 80
-static_assert(F0_CI % 32 == 16 && F1_CI % 32 == 16 && F2_CI % 32 == 16, "bank-conflict-free pitches");
+constexpr int I0_CIP = 20, I1_CIP = 36, I2_CIP = 68;                 // elements
+constexpr int I0_TP = 66, I1_TP = 34, I2_TP = 18;                    // t positions incl. zero guards
+// fp32 images (float units)
 constexpr int kF0Off = kImgOff;
-constexpr int kF1Off = kF0Off + 16 * F0_CI;
-constexpr int kF2Off = kF1Off + 32 * F1_CI;
-constexpr int kImgEnd = kF2Off + 64 * F2_CI;
-// bf16 images [clip][t][ci], ci pitch = Cin + 4 (t stride of 10 / 18 / 34
-// dwords: the 16 t-lanes of a B-fragment read hit distinct bank pairs).
-constexpr int B0_CIP = 20, B1_CIP = 36, B2_CIP = 68;                 // uint16 units
-constexpr int B0_TP = 66, B1_TP = 34, B2_TP = 18;                    // t positions incl. guards
-constexpr int kB0Off = kImgOff;                                      // float units
-constexpr int kB1Off = kB0Off + NBF * B0_TP * B0_CIP / 2;
-constexpr int kB2Off = kB1Off + NBF * B1_TP * B1_CIP / 2;
-static_assert(kB2Off + NBF * B2_TP * B2_CIP / 2 <= kImgEnd, "bf16 images overlay the fp32 region");
-static_assert((kB1Off % 2) == 0 && (kB2Off % 2) == 0, "8-byte aligned bf16 images");
+constexpr int kF1Off = kF0Off + NBF * I0_TP * I0_CIP;
+constexpr int kF2Off = kF1Off + NBF * I1_TP * I1_CIP;
+constexpr int kImgEnd = kF2Off + NBF * I2_TP * I2_CIP;
+// bf16 images (offsets in float units)
+constexpr int kB0Off = kImgOff;
+constexpr int kB1Off = kB0Off + NBF * I0_TP * I0_CIP / 2;
+constexpr int kB2Off = kB1Off + NBF * I1_TP * I1_CIP / 2;
+static_assert(kF1Off % 4 == 0 && kF2Off % 4 == 0 && kB1Off % 2 == 0 && kB2Off % 2 == 0, "vector-aligned images");
 constexpr int kFusedLds = kImgEnd;
 static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 
@@ -252,8 +246,8 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         if (!(exp_flags & 2)) spin_until(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
         const float* lrow = (i & 1 ? L1 : L) + ln;
         const int k = (cw + 3 * s) & 7;
-        float* f0 = F0 + s * F0_CLIP + 1 + ln;
-        uint16_t* f0b = B0 + (s * B0_TP + 1 + ln) * B0_CIP;
+        float* f0 = F0 + (s * I0_TP + 1 + ln) * I0_CIP;
+        uint16_t* f0b = B0 + (s * I0_TP + 1 + ln) * I0_CIP;
         float* fo = feats_out ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) + ln : nullptr;
         if (k < 5) {
           const int c0 = 2 * k;
@@ -262,8 +256,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
           if (valid && BF) {
             *reinterpret_cast<uint32_t*>(f0b + c0) = bf16_bits(y0) | (bf16_bits(y1) << 16);   // c0 even
           } else if (valid) {
-            f0[c0 * F0_CI] = y0;
-            f0[(c0 + 1) * F0_CI] = y1;
+            *reinterpret_cast<float2*>(f0 + c0) = make_float2(y0, y1);   // c0 even
           }
           if (valid) {
             if (fo) {
@@ -275,7 +268,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
           const int c0 = k + 5;
           const float y = cmvn_lane(dct_coef<true>(c0, lrow), valid, kNFramesB);
           if (valid) {
-            if (BF) f0b[c0] = (uint16_t)bf16_bits(y); else f0[c0 * F0_CI] = y;
+            if (BF) f0b[c0] = (uint16_t)bf16_bits(y); else f0[c0] = y;
             if (fo) fo[c0 * kNFramesB] = y;
           }
         }
@@ -288,20 +281,19 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     // conv1: co tile (cw&1), clip (cw>>1), 4 t-tiles.
     {
       const int co0 = 16 * (cw & 1), cl = cw >> 1;
-      const int bo = lk * F0_CI + li + cl * F0_CLIP;
+      const int bo = (cl * I0_TP + li) * I0_CIP + 4 * lk;   // this lane's element in the [clip][t][ci] image
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int ta = 32 * p, tb = ta + 16;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
         if constexpr (BF) {
-          const int bb = (cl * B0_TP + li) * B0_CIP + 4 * lk;
-          conv_pair_bf<3, 1, B0_CIP>(B0, w1b, bb + ta * B0_CIP, bb + tb * B0_CIP, acc_a, acc_b);
-          epi_pool_bf<B1_CIP, B1_TP, 31>(acc_a, B1, co0, cl, ta, lane);
-          epi_pool_bf<B1_CIP, B1_TP, 31>(acc_b, B1, co0, cl, tb, lane);
+          conv_pair_bf<3, 1, I0_CIP>(B0, w1b, bo + ta * I0_CIP, bo + tb * I0_CIP, acc_a, acc_b);
+          epi_pool_bf<I1_CIP, I1_TP, 31>(acc_a, B1, co0, cl, ta, lane);
+          epi_pool_bf<I1_CIP, I1_TP, 31>(acc_b, B1, co0, cl, tb, lane);
         } else {
-          conv_pair<12, F0_CI, 4, 6>(F0, w1, bo + ta, bo + tb, acc_a, acc_b);
-          epi_pool<F1_CI, F1_CLIP, 31>(acc_a, F1, co0, cl, ta, lane);
-          epi_pool<F1_CI, F1_CLIP, 31>(acc_b, F1, co0, cl, tb, lane);
+          conv_pair_v<1, I0_CIP, 1>(F0, w1, bo + ta * I0_CIP, bo + tb * I0_CIP, acc_a, acc_b);
+          epi_pool_v<I1_CIP, I1_TP, 31>(acc_a, F1, co0, cl, ta, lane);
+          epi_pool_v<I1_CIP, I1_TP, 31>(acc_b, F1, co0, cl, tb, lane);
         }
       }
     }
@@ -318,11 +310,11 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
-        const int bb = (cl * B1_TP + li) * B1_CIP + 4 * lk;
+        const int bb = (cl * I1_TP + li) * I1_CIP + 4 * lk;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
-        conv_pair_bf<6, 2, B1_CIP>(B1, w2b, bb, bb + 16 * B1_CIP, acc_a, acc_b);
-        epi_pool_bf<B2_CIP, B2_TP, 15>(acc_a, B2, co0, cl, 0, lane);
-        epi_pool_bf<B2_CIP, B2_TP, 15>(acc_b, B2, co0, cl, 16, lane);
+        conv_pair_bf<6, 2, I1_CIP>(B1, w2b, bb, bb + 16 * I1_CIP, acc_a, acc_b);
+        epi_pool_bf<I2_CIP, I2_TP, 15>(acc_a, B2, co0, cl, 0, lane);
+        epi_pool_bf<I2_CIP, I2_TP, 15>(acc_b, B2, co0, cl, 16, lane);
       }
     } else {
       float w2[24];
@@ -332,11 +324,11 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
-        const int bo = lk * F1_CI + li + cl * F1_CLIP;
+        const int bo = (cl * I1_TP + li) * I1_CIP + 4 * lk;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
-        conv_pair<24, F1_CI, 8, 8>(F1, w2, bo, bo + 16, acc_a, acc_b);
-        epi_pool<F2_CI, F2_CLIP, 15>(acc_a, F2, co0, cl, 0, lane);
-        epi_pool<F2_CI, F2_CLIP, 15>(acc_b, F2, co0, cl, 16, lane);
+        conv_pair_v<2, I1_CIP, 2>(F1, w2, bo, bo + 16 * I1_CIP, acc_a, acc_b);
+        epi_pool_v<I2_CIP, I2_TP, 15>(acc_a, F2, co0, cl, 0, lane);
+        epi_pool_v<I2_CIP, I2_TP, 15>(acc_b, F2, co0, cl, 16, lane);
       }
     }
     WK_STAMP(3);
@@ -346,16 +338,15 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     // conv3: co tile cw, the 4 clips; GAP -> G[128][4].
     {
       const int co0 = 16 * cw;
-      const int bo = lk * F2_CI + li;
+      const int bo = li * I2_CIP + 4 * lk;
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int ca = 2 * p, cb = 2 * p + 1;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
         if constexpr (BF) {
-          const int bb = li * B2_CIP + 4 * lk;
-          conv_pair_bf<12, 4, B2_CIP, 6>(B2, w3b, bb + ca * B2_TP * B2_CIP, bb + cb * B2_TP * B2_CIP, acc_a, acc_b);
+          conv_pair_bf<12, 4, I2_CIP, 6>(B2, w3b, bo + ca * I2_TP * I2_CIP, bo + cb * I2_TP * I2_CIP, acc_a, acc_b);
         } else {
-          conv_pair<48, F2_CI, 16, 8>(F2, w3, bo + ca * F2_CLIP, bo + cb * F2_CLIP, acc_a, acc_b);
+          conv_pair_v<4, I2_CIP, 2>(F2, w3, bo + ca * I2_TP * I2_CIP, bo + cb * I2_TP * I2_CIP, acc_a, acc_b);
         }
         epi_gap<NBF>(acc_a, Gp, co0, ca, lane);
         epi_gap<NBF>(acc_b, Gp, co0, cb, lane);

@@ -66,11 +66,13 @@ constexpr int kOffF1 = kOffW3 + 128 * 64 * 3;   // classifier.0.weight [64][128]
 constexpr int kOffF2 = kOffF1 + 64 * 128;       // classifier.2.weight [1][64]
 constexpr int kNumWeights = kOffF2 + 64;        // 40224
 
-// Fragment-major copy of the weights for the MFMA kernels: for each 16-row
-// output tile and k-step s (k = 4s..4s+3), the 64 values lane l feeds as the
-// A operand of v_mfma_f32_16x16x4_f32 (row = l&15, k = 4s + (l>>4)), so a
-// wave loads one fragment with one coalesced 256-byte load.
-//   conv k order: k = tap*Cin_pad + ci  (Cin_pad = 16 for conv1, zero rows)
+// Fragment-major copy of the weights for the MFMA kernels.  Per 16-row output
+// tile and k-step, the 64 values lane l feeds as the A operand of
+// v_mfma_f32_16x16x4_f32 (row = l&15), so a wave loads one fragment with one
+// coalesced 256-byte load.
+//   conv ([clip][t][ci] images): step s = 4 (tap * CB + cb) + j, lane group
+//     q = l>>4 feeds ci = 16 cb + 4 q + j at that tap (Cin padded to 16).
+//   classifier.0: k = 4s + q.
 constexpr int kPkW1 = 0;                        // [2 tiles][12 s][64]
 constexpr int kPkW2 = kPkW1 + 2 * 12 * 64;      // [4][24][64]
 constexpr int kPkW3 = kPkW2 + 4 * 24 * 64;      // [8][48][64]
@@ -111,26 +113,21 @@ inline void pack_fragments_bf16(const float* w, uint16_t* pk) {
   pack(kPbW3, 8, 64, 64, kOffW3);
 }
 
-// Host-side packing of the WK_NUM_WEIGHTS blob into the fragment-major layout.
+// Host-side packing of the WK_NUM_WEIGHTS blob into the fragment-major layouts.
 inline void pack_fragments(const float* w, float* pk) {
-  for (int t = 0; t < 2; ++t)
-    for (int s = 0; s < 12; ++s)
-      for (int l = 0; l < 64; ++l) {
-        const int co = 16 * t + (l & 15), ci = 4 * (s & 3) + (l >> 4), tap = s >> 2;
-        pk[kPkW1 + (t * 12 + s) * 64 + l] = ci < 13 ? w[kOffW1 + (co * 13 + ci) * 3 + tap] : 0.0f;
-      }
-  for (int t = 0; t < 4; ++t)
-    for (int s = 0; s < 24; ++s)
-      for (int l = 0; l < 64; ++l) {
-        const int co = 16 * t + (l & 15), ci = 4 * (s & 7) + (l >> 4), tap = s >> 3;
-        pk[kPkW2 + (t * 24 + s) * 64 + l] = w[kOffW2 + (co * 32 + ci) * 3 + tap];
-      }
-  for (int t = 0; t < 8; ++t)
-    for (int s = 0; s < 48; ++s)
-      for (int l = 0; l < 64; ++l) {
-        const int co = 16 * t + (l & 15), ci = 4 * (s & 15) + (l >> 4), tap = s >> 4;
-        pk[kPkW3 + (t * 48 + s) * 64 + l] = w[kOffW3 + (co * 64 + ci) * 3 + tap];
-      }
+  auto conv_blocked = [&](int off, int tiles, int cin, int cin_pad, int wbase) {
+    const int cb_n = cin_pad / 16, nsteps = 12 * cb_n;
+    for (int t = 0; t < tiles; ++t)
+      for (int s = 0; s < nsteps; ++s)
+        for (int l = 0; l < 64; ++l) {
+          const int g = s >> 2, j = s & 3, tap = g / cb_n, cb = g % cb_n;
+          const int co = 16 * t + (l & 15), ci = 16 * cb + 4 * (l >> 4) + j;
+          pk[off + (t * nsteps + s) * 64 + l] = ci < cin ? w[wbase + (co * cin + ci) * 3 + tap] : 0.0f;
+        }
+  };
+  conv_blocked(kPkW1, 2, 13, 16, kOffW1);
+  conv_blocked(kPkW2, 4, 32, 32, kOffW2);
+  conv_blocked(kPkW3, 8, 64, 64, kOffW3);
   for (int t = 0; t < 4; ++t)
     for (int s = 0; s < 32; ++s)
       for (int l = 0; l < 64; ++l) {
