@@ -74,9 +74,9 @@ def cpu_baseline(seconds: float):
                       f"+ LightweightKWS on the xiaoa.onnx weights (oracle/wk_torch_cpu.py)"}
 
 
-def load_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
-    p = os.path.join(REPO, "profiles", "hbm_traffic.json")
+def load_traffic(precision="fp32"):
+    """HBM bytes per window from the committed rocprofv3 PMC summary of this precision, if any."""
+    p = os.path.join(REPO, "profiles", "hbm_traffic.json" if precision == "fp32" else f"hbm_traffic_{precision}.json")
     try:
         with open(p) as fh:
             d = json.load(fh)
@@ -151,7 +151,7 @@ def main():
         total = world * B * args.steps
         value = total / elapsed
         achieved = FLOP_PER_WINDOW * B / (launch_ms * 1e-3) / 1e12
-        traffic_bpw, traffic_src = load_traffic()
+        traffic_bpw, traffic_src = load_traffic(args.precision)
         out = {
             "metric": "audio windows/sec (1s@16kHz, 40-MFCC) through xiaoa CNN at 1/2/4/8 MI355X",
             "value": round(value, 1),
