@@ -33,6 +33,16 @@ PEAK_FP32_TFLOPS = 157.3               # MI355X fp32 vector == fp32 MFMA (MI355X
 PEAK_HBM_GBS = 8000.0
 
 
+# --precision -> (dtype, workload) of the bench line
+PRECISIONS = {
+    "fp32": ("f32", "config2: fused MFCC(torchaudio+CMVN)+xiaoa CNN fp32, B clips per GPU"),
+    "bf16": ("bf16 convolutions, f32 front-end/classifier",
+             "config4: fused MFCC(torchaudio+CMVN) fp32 + xiaoa CNN bf16, B clips per GPU"),
+    "bf16x3": ("f32-grade convolutions as split bf16 (hi*hi + hi*lo + lo*hi, f32 accumulate), f32 front-end/classifier",
+               "config2: fused MFCC(torchaudio+CMVN)+xiaoa CNN at the fp32 logit tolerance, B clips per GPU"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -42,8 +52,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
-                    help="CNN convolutions: fp32 (config 2, default) or bf16 (config 4); front-end fp32 either way")
+    ap.add_argument("--precision", default="fp32", choices=list(PRECISIONS),
+                    help="CNN convolutions: fp32 MFMA (config 2, default), bf16 (config 4), or bf16x3 "
+                         "(config 2 at fp32-grade accuracy on split-bf16 MFMA); front-end fp32 always")
     return ap.parse_args()
 
 
@@ -163,12 +174,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32" if args.precision == "fp32" else "bf16 convolutions, f32 front-end/classifier",
+            "dtype": PRECISIONS[args.precision][0],
             "data": "synthetic: device counter-hash generator, clamp(0.1*N(0,1))+440 Hz sine on odd clips "
                     "(SURVEY 8(d) config 2); xiaoa.onnx weights",
-            "config": {"workload": ("config2: fused MFCC(torchaudio+CMVN)+xiaoa CNN fp32, B clips per GPU"
-                                    if args.precision == "fp32" else
-                                    "config4: fused MFCC(torchaudio+CMVN) fp32 + xiaoa CNN bf16, B clips per GPU"),
+            "config": {"workload": PRECISIONS[args.precision][1],
                        "batch_per_gpu": B, "global_batch": world * B, "seq_len": 16000,
                        "parallelism": f"dp{world} (per-rank clip split, no collectives)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,

@@ -18,7 +18,7 @@ struct wk_handle {
   float* d_packed;       // fragment-major weights (wk::pack_fragments) for the fused kernel
   float* d_feats_ws;     // feature workspace for the unfused path
   int8_t* d_int8;        // int8 weights (WK_PREC_INT8, wk::quantize_int8_weights)
-  uint16_t* d_bf16;      // bf16 conv fragments (WK_PREC_BF16, wk::pack_fragments_bf16)
+  uint16_t* d_bf16;      // bf16 conv fragments (WK_PREC_BF16; BF16X3: hi then lo, wk::pack_fragments_bf16)
   int64_t ws_clips;
   int unfused;           // WAKEWORD_UNFUSED=1: front-end + CNN as two kernels (A/B testing)
   int fused_exp;         // WAKEWORD_FUSED_EXP: role-isolation timing experiments (wrong logits)
@@ -77,7 +77,8 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
   if (!cfg || !out) return invalid("wk_create: null cfg/out");
   *out = nullptr;
   if (cfg->mode != WK_MODE_TORCHAUDIO_CMVN && cfg->mode != WK_MODE_ESP_MFCC) return invalid("wk_create: bad mode");
-  if (cfg->precision != WK_PREC_FP32 && cfg->precision != WK_PREC_BF16 && cfg->precision != WK_PREC_INT8)
+  if (cfg->precision != WK_PREC_FP32 && cfg->precision != WK_PREC_BF16 && cfg->precision != WK_PREC_INT8 &&
+      cfg->precision != WK_PREC_BF16X3)
     return invalid("wk_create: bad precision");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
@@ -110,9 +111,11 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
       if ((e2 = hipMemcpy(h->d_packed, pk.data(), sizeof(float) * wk::kNumPacked, hipMemcpyHostToDevice)) !=
           hipSuccess)
         return hip_fail(e2, "hipMemcpy(packed weights)");
-      if (cfg->precision == WK_PREC_BF16) {
-        std::vector<uint16_t> pb(wk::kNumPackedBf16);
+      if (cfg->precision == WK_PREC_BF16 || cfg->precision == WK_PREC_BF16X3) {
+        const bool split = cfg->precision == WK_PREC_BF16X3;   // hi fragments, then lo fragments
+        std::vector<uint16_t> pb(wk::kNumPackedBf16 * (split ? 2 : 1));
         wk::pack_fragments_bf16(host_weights, pb.data());
+        if (split) wk::pack_fragments_bf16(host_weights, pb.data() + wk::kNumPackedBf16, true);
         if ((e2 = hipMalloc(&h->d_bf16, pb.size() * 2)) != hipSuccess) return hip_fail(e2, "hipMalloc(bf16 weights)");
         if ((e2 = hipMemcpy(h->d_bf16, pb.data(), pb.size() * 2, hipMemcpyHostToDevice)) != hipSuccess)
           return hip_fail(e2, "hipMemcpy(bf16 weights)");
@@ -182,7 +185,7 @@ wk_status wk_cnn(wk_handle* h, const float* d_feats, int64_t batch, float* d_log
   if (!h) return invalid("wk_cnn: null handle");
   if (!h->d_weights) return invalid("wk_cnn: handle created without weights");
   if (batch < 0 || (batch > 0 && (!d_feats || !d_logits))) return invalid("wk_cnn: bad arguments");
-  if (h->cfg.precision == WK_PREC_BF16) {
+  if (h->cfg.precision == WK_PREC_BF16 || h->cfg.precision == WK_PREC_BF16X3) {
     g_last_error = "wk_cnn: bf16 convolutions run inside the fused kernel only (use wk_forward)";
     return WK_ERR_UNSUPPORTED;
   }
@@ -208,8 +211,9 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
   const bool int8 = h->cfg.precision == WK_PREC_INT8;
   return on_device(h->cfg.device, [&]() -> wk_status {
     if ((!h->unfused && !int8) || h->d_bf16) {   // bf16 convolutions exist only in the fused kernel
+      const int conv_mode = h->cfg.precision == WK_PREC_BF16 ? 1 : (h->cfg.precision == WK_PREC_BF16X3 ? 2 : 0);
       hipError_t e = wk::launch_fused(dtype == WK_DTYPE_I16, d_audio, batch, clip_stride, h->d_packed, h->d_bf16,
-                                      d_logits, d_feats_or_null, h->n_cu, (hipStream_t)stream, h->fused_exp);
+                                      conv_mode, d_logits, d_feats_or_null, h->n_cu, (hipStream_t)stream, h->fused_exp);
       return e == hipSuccess ? WK_OK : hip_fail(e, "fused launch");
     }
     const size_t esz = dtype == WK_DTYPE_I16 ? 2 : 4;

@@ -115,6 +115,57 @@ __device__ __forceinline__ void epi_pool_bf(const f32x4& acc, uint16_t* __restri
   }
 }
 
+// ---- split-bf16 ("bf16x3") convolutions: fp32-grade products at bf16 MFMA rate.
+// x = xh + xl and w = wh + wl with xh = bf16(x), xl = bf16(x - xh) (both RNE);
+// x w ~= xh wh + (xl wh + xh wl), dropping xl wl (relative 2^-16).  Each bf16
+// product is exact in the fp32 accumulator, so the per-product error is
+// ~2^-16 relative -- three v_mfma_f32_16x16x16_bf16 (8 passes each) in place
+// of four v_mfma_f32_16x16x4f32 (fp32 MFMA: 1/16 the bf16 rate).  Images hold
+// xh at ci and xl at ci + LO (LO = 16 CB) of the same t row; the cross terms
+// go to separate accumulators (summed by the caller) to space dependent MFMAs.
+template <int NSTEP, int CB, int CIP, int CHUNK = 0>
+__device__ __forceinline__ void conv_pair_bf3(const uint16_t* __restrict__ img, const s4 (&wh)[NSTEP],
+                                              const s4 (&wl)[NSTEP], int boff_a, int boff_b, f32x4& acc_a,
+                                              f32x4& acc_b, f32x4& x_a, f32x4& x_b) {
+  constexpr int LO = 16 * CB;
+#pragma unroll
+  for (int s = 0; s < NSTEP; ++s) {
+    const int off = (s / CB) * CIP + 16 * (s % CB);
+    const s4 ha = *reinterpret_cast<const s4*>(img + boff_a + off);
+    const s4 hb = *reinterpret_cast<const s4*>(img + boff_b + off);
+    const s4 la = *reinterpret_cast<const s4*>(img + boff_a + off + LO);
+    const s4 lb = *reinterpret_cast<const s4*>(img + boff_b + off + LO);
+    acc_a = mfma_bf16(wh[s], ha, acc_a);
+    acc_b = mfma_bf16(wh[s], hb, acc_b);
+    x_a = mfma_bf16(wl[s], ha, x_a);
+    x_b = mfma_bf16(wl[s], hb, x_b);
+    x_a = mfma_bf16(wh[s], la, x_a);
+    x_b = mfma_bf16(wh[s], lb, x_b);
+    if (CHUNK > 0 && (s % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// epi_pool_bf for split images: xh (8 bytes at co) and xl (8 bytes at co + LO).
+template <int CIP_N, int TP_N, int TN, int LO>
+__device__ __forceinline__ void epi_pool_bf3(const f32x4& acc, uint16_t* __restrict__ next, int co0, int clip, int t0,
+                                             int lane) {
+  const int t = t0 + (lane & 15);
+  const int tp = t >> 1;
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float x = fmaxf(acc[r], 0.0f);
+    const float v = fmaxf(x, swap_adjacent(x));
+    h[r] = bf16_bits(v);
+    l[r] = bf16_bits(v - __uint_as_float(h[r] << 16));
+  }
+  if (!(lane & 1) && tp < TN) {
+    uint16_t* p = next + (clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4);
+    *reinterpret_cast<uint2*>(p) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    *reinterpret_cast<uint2*>(p + LO) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+  }
+}
+
 // ---- fp32 convolutions from [clip][t][ci] images (ci-blocked K order) ----
 // MFMA K order is free as long as A and B agree: lane group q = lane >> 4
 // takes ci = 16 cb + 4 q + j at step (tap, cb, j), so the B values of 4

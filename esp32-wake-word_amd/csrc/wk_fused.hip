@@ -43,15 +43,21 @@ constexpr int NBF = 4;               // clips per CNN batch
 constexpr int kFusedBlock = 1024;    // 8 front-end + 8 CNN waves
 // LDS carve after the front-end's (wk_fe_dev.h): fixed tail, then the CNN
 // images [clip][t][ci] -- fp32, or bf16 for bf16 convolutions -- overlaying
-// one region.  ci pitch = Cin + 4 elements: the 16 t-lanes of a B-fragment
-// read (16 B fp32 / 8 B bf16 per lane) land on distinct bank groups.
+// one region.  ci pitch = 8 mod 16 elements: the 16 t-lanes of each lane
+// group of a B-fragment read (ds_read_b128 fp32 / ds_read_b64 bf16) and of the
+// pooled stores land on distinct banks.
 constexpr int kGOff = kFeLds;                       // pooled features [128][4]
 constexpr int kFcpOff = kGOff + 128 * NBF;          // classifier.0 partials [2][64][4]
 constexpr int kL1Off = kFcpOff + 2 * 64 * NBF;      // second log-mel buffer [40][64] (first: kLOff)
 constexpr int kCtrlOff = kL1Off + kLSize;           // control words
 constexpr int kImgOff = (kCtrlOff + 16 + 3) & ~3;   // 16-byte aligned
-constexpr int I0_CIP = 20, I1_CIP = 36, I2_CIP = 68;                 // elements
-constexpr int I0_TP = 66, I1_TP = 34, I2_TP = 18;                    // t positions incl. zero guards
+constexpr int I0_CIP = 24, I1_CIP = 40, I2_CIP = 72;                 // elements (= 8 mod 16)
+// t rows: row 0 is the left zero guard, rows 1..L hold the L frames.  No right
+// guard: every layer's length L is odd, so maxpool(2) drops the one output
+// that would read it; the dropped outputs' reads of rows L+1, L+2 land in the
+// next clip's (or the next image's) rows, which only affects their own MFMA
+// columns.  conv3 keeps 2 spare rows so its last clip stays inside the carve.
+constexpr int I0_TP = 64, I1_TP = 32, I2_TP = 18;
 // fp32 images (float units)
 constexpr int kF0Off = kImgOff;
 constexpr int kF1Off = kF0Off + NBF * I0_TP * I0_CIP;
@@ -61,7 +67,15 @@ constexpr int kImgEnd = kF2Off + NBF * I2_TP * I2_CIP;
 constexpr int kB0Off = kImgOff;
 constexpr int kB1Off = kB0Off + NBF * I0_TP * I0_CIP / 2;
 constexpr int kB2Off = kB1Off + NBF * I1_TP * I1_CIP / 2;
-static_assert(kF1Off % 4 == 0 && kF2Off % 4 == 0 && kB1Off % 2 == 0 && kB2Off % 2 == 0, "vector-aligned images");
+// split-bf16 images (WK_PREC_BF16X3): xh at ci, xl at ci + 16 CB of the same row
+constexpr int X0_CIP = 40, X1_CIP = 72, X2_CIP = 136;                // halfs (= 8 mod 16)
+constexpr int kX0Off = kImgOff;
+constexpr int kX1Off = kX0Off + NBF * I0_TP * X0_CIP / 2;
+constexpr int kX2Off = kX1Off + NBF * I1_TP * X1_CIP / 2;
+static_assert(kX2Off + NBF * I2_TP * X2_CIP / 2 <= kImgEnd, "split images fit the fp32 carve");
+static_assert(kF1Off % 4 == 0 && kF2Off % 4 == 0 && kB1Off % 2 == 0 && kB2Off % 2 == 0 && kX1Off % 2 == 0 &&
+                  kX2Off % 2 == 0, "vector-aligned images");
+enum { kConvF32 = 0, kConvBf16 = 1, kConvBf16x3 = 2 };
 constexpr int kFusedLds = kImgEnd;
 static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 
@@ -183,7 +197,7 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
 // ---------------------------------------------------------------------------
 // CNN role (waves 8-15): batches of NBF clips from the conv1 image.
 // ---------------------------------------------------------------------------
-template <bool BF>
+template <int CM>   // kConvF32 / kConvBf16 / kConvBf16x3
 __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ pk, const uint16_t* __restrict__ pkb,
                                          int64_t n_mine, float* __restrict__ logits, float* __restrict__ feats_out,
                                          int cw, int lane, int exp_flags) {
@@ -195,7 +209,12 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   uint16_t* B0 = reinterpret_cast<uint16_t*>(smem + kB0Off);
   uint16_t* B1 = reinterpret_cast<uint16_t*>(smem + kB1Off);
   uint16_t* B2 = reinterpret_cast<uint16_t*>(smem + kB2Off);
-  const auto rsb = make_rsrc(pkb, 2 * kNumPackedBf16);
+  uint16_t* X0 = reinterpret_cast<uint16_t*>(smem + kX0Off);
+  uint16_t* X1 = reinterpret_cast<uint16_t*>(smem + kX1Off);
+  uint16_t* X2 = reinterpret_cast<uint16_t*>(smem + kX2Off);
+  constexpr bool BF = CM == kConvBf16, X3 = CM == kConvBf16x3;
+  constexpr int kLoW = kNumPackedBf16;   // the xl fragments follow the xh ones (pack_fragments_bf16x3)
+  const auto rsb = make_rsrc(pkb, 2 * kNumPackedBf16 * (X3 ? 2 : 1));
   auto frag_bf = [&](int elem_off) -> s4 {   // one lane's 4 bf16 of the fragment at elem_off (x 64 lanes x 4)
     return __builtin_bit_cast(s4, __builtin_amdgcn_raw_buffer_load_b64(rsb, 8 * lane, 2 * elem_off, 0));
   };
@@ -213,10 +232,11 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   // other layers' are re-read from L2 per batch.
   float w3[48];
   s4 w3b[12];
-  if constexpr (BF) {
+  if constexpr (BF || X3) {
 #pragma unroll
     for (int s = 0; s < 12; ++s) w3b[s] = frag_bf(kPbW3 + (cw * 12 + s) * 256);
-  } else {
+  }
+  if constexpr (CM == kConvF32) {
 #pragma unroll
     for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
   }
@@ -224,11 +244,16 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   WK_STAMP_INIT
   for (int64_t b = 0; b < n_batches; ++b) {
     float w1[12];
-    s4 w1b[3];
-    if constexpr (BF) {
+    s4 w1b[3], w1l[3];
+    if constexpr (BF || X3) {
 #pragma unroll
       for (int s = 0; s < 3; ++s) w1b[s] = frag_bf(kPbW1 + ((cw & 1) * 3 + s) * 256);
-    } else {
+    }
+    if constexpr (X3) {
+#pragma unroll
+      for (int s = 0; s < 3; ++s) w1l[s] = frag_bf(kLoW + kPbW1 + ((cw & 1) * 3 + s) * 256);
+    }
+    if constexpr (CM == kConvF32) {
 #pragma unroll
       for (int s = 0; s < 12; ++s) w1[s] = buf_load(rs, lv, 4 * (kPkW1 + ((cw & 1) * 12 + s) * 64));
     }
@@ -248,6 +273,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         const int k = (cw + 3 * s) & 7;
         float* f0 = F0 + (s * I0_TP + 1 + ln) * I0_CIP;
         uint16_t* f0b = B0 + (s * I0_TP + 1 + ln) * I0_CIP;
+        uint16_t* f0x = X0 + (s * I0_TP + 1 + ln) * X0_CIP;
         float* fo = feats_out ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) + ln : nullptr;
         if (k < 5) {
           const int c0 = 2 * k;
@@ -255,6 +281,11 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
           cmvn_lane2(y0, y1, valid, kNFramesB);
           if (valid && BF) {
             *reinterpret_cast<uint32_t*>(f0b + c0) = bf16_bits(y0) | (bf16_bits(y1) << 16);   // c0 even
+          } else if (valid && X3) {
+            const uint32_t h0 = bf16_bits(y0), h1 = bf16_bits(y1);
+            *reinterpret_cast<uint32_t*>(f0x + c0) = h0 | (h1 << 16);
+            *reinterpret_cast<uint32_t*>(f0x + 16 + c0) =
+                bf16_bits(y0 - __uint_as_float(h0 << 16)) | (bf16_bits(y1 - __uint_as_float(h1 << 16)) << 16);
           } else if (valid) {
             *reinterpret_cast<float2*>(f0 + c0) = make_float2(y0, y1);   // c0 even
           }
@@ -268,7 +299,15 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
           const int c0 = k + 5;
           const float y = cmvn_lane(dct_coef<true>(c0, lrow), valid, kNFramesB);
           if (valid) {
-            if (BF) f0b[c0] = (uint16_t)bf16_bits(y); else f0[c0] = y;
+            if (BF) {
+              f0b[c0] = (uint16_t)bf16_bits(y);
+            } else if (X3) {
+              const uint32_t h = bf16_bits(y);
+              f0x[c0] = (uint16_t)h;
+              f0x[16 + c0] = (uint16_t)bf16_bits(y - __uint_as_float(h << 16));
+            } else {
+              f0[c0] = y;
+            }
             if (fo) fo[c0 * kNFramesB] = y;
           }
         }
@@ -290,6 +329,12 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
           conv_pair_bf<3, 1, I0_CIP>(B0, w1b, bo + ta * I0_CIP, bo + tb * I0_CIP, acc_a, acc_b);
           epi_pool_bf<I1_CIP, I1_TP, 31>(acc_a, B1, co0, cl, ta, lane);
           epi_pool_bf<I1_CIP, I1_TP, 31>(acc_b, B1, co0, cl, tb, lane);
+        } else if constexpr (X3) {
+          const int bx = (cl * I0_TP + li) * X0_CIP + 4 * lk;
+          f32x4 x_a = {0, 0, 0, 0}, x_b = {0, 0, 0, 0};
+          conv_pair_bf3<3, 1, X0_CIP>(X0, w1b, w1l, bx + ta * X0_CIP, bx + tb * X0_CIP, acc_a, acc_b, x_a, x_b);
+          epi_pool_bf3<X1_CIP, I1_TP, 31, 32>(acc_a + x_a, X1, co0, cl, ta, lane);
+          epi_pool_bf3<X1_CIP, I1_TP, 31, 32>(acc_b + x_b, X1, co0, cl, tb, lane);
         } else {
           conv_pair_v<1, I0_CIP, 1>(F0, w1, bo + ta * I0_CIP, bo + tb * I0_CIP, acc_a, acc_b);
           epi_pool_v<I1_CIP, I1_TP, 31>(acc_a, F1, co0, cl, ta, lane);
@@ -315,6 +360,22 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         conv_pair_bf<6, 2, I1_CIP>(B1, w2b, bb, bb + 16 * I1_CIP, acc_a, acc_b);
         epi_pool_bf<I2_CIP, I2_TP, 15>(acc_a, B2, co0, cl, 0, lane);
         epi_pool_bf<I2_CIP, I2_TP, 15>(acc_b, B2, co0, cl, 16, lane);
+      }
+    } else if constexpr (X3) {
+      s4 w2b[6], w2l[6];
+#pragma unroll
+      for (int s = 0; s < 6; ++s) w2b[s] = frag_bf(kPbW2 + ((cw & 3) * 6 + s) * 256);
+#pragma unroll
+      for (int s = 0; s < 6; ++s) w2l[s] = frag_bf(kLoW + kPbW2 + ((cw & 3) * 6 + s) * 256);
+      const int co0 = 16 * (cw & 3);
+#pragma unroll 1
+      for (int p = 0; p < 2; ++p) {
+        const int cl = 2 * (cw >> 2) + p;
+        const int bb = (cl * I1_TP + li) * X1_CIP + 4 * lk;
+        f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0}, x_a = {0, 0, 0, 0}, x_b = {0, 0, 0, 0};
+        conv_pair_bf3<6, 2, X1_CIP>(X1, w2b, w2l, bb, bb + 16 * X1_CIP, acc_a, acc_b, x_a, x_b);
+        epi_pool_bf3<X2_CIP, I2_TP, 15, 64>(acc_a + x_a, X2, co0, cl, 0, lane);
+        epi_pool_bf3<X2_CIP, I2_TP, 15, 64>(acc_b + x_b, X2, co0, cl, 16, lane);
       }
     } else {
       float w2[24];
@@ -345,6 +406,16 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
         if constexpr (BF) {
           conv_pair_bf<12, 4, I2_CIP, 6>(B2, w3b, bo + ca * I2_TP * I2_CIP, bo + cb * I2_TP * I2_CIP, acc_a, acc_b);
+        } else if constexpr (X3) {
+          s4 w3l[12];   // the lo parts are re-read from L2 per pass (VGPR budget)
+#pragma unroll
+          for (int s = 0; s < 12; ++s) w3l[s] = frag_bf(kLoW + kPbW3 + (cw * 12 + s) * 256);
+          const int bx = li * X2_CIP + 4 * lk;
+          f32x4 x_a = {0, 0, 0, 0}, x_b = {0, 0, 0, 0};
+          conv_pair_bf3<12, 4, X2_CIP, 3>(X2, w3b, w3l, bx + ca * I2_TP * X2_CIP, bx + cb * I2_TP * X2_CIP, acc_a,
+                                          acc_b, x_a, x_b);
+          acc_a += x_a;
+          acc_b += x_b;
         } else {
           conv_pair_v<4, I2_CIP, 2>(F2, w3, bo + ca * I2_TP * I2_CIP, bo + cb * I2_TP * I2_CIP, acc_a, acc_b);
         }
@@ -402,7 +473,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   WK_STAMP_FLUSH(8 + cw);
 }
 
-template <typename T, bool BF>
+template <typename T, int CM>
 __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __restrict__ audio, int64_t batch,
                                                                  int64_t clip_stride, const float* __restrict__ wts,
                                                                  const uint16_t* __restrict__ wbf,
@@ -422,7 +493,7 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
 #endif
   } else {
 #ifndef WK_EXPERIMENT_NO_CNN
-    if (!(exp_flags & 1)) cnn_role<BF>(smem, wts, wbf, n_mine, logits, feats_out, wave - 8, lane, exp_flags);
+    if (!(exp_flags & 1)) cnn_role<CM>(smem, wts, wbf, n_mine, logits, feats_out, wave - 8, lane, exp_flags);
 #endif
   }
 }
@@ -443,23 +514,25 @@ extern "C" int wk_debug_stamps(unsigned long long* host_out, int reset) {
 namespace wk {
 
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
-                        const uint16_t* wbf, float* logits, float* feats_or_null, int grid_cap, hipStream_t stream,
-                        int exp_flags) {
+                        const uint16_t* wbf, int conv_mode, float* logits, float* feats_or_null, int grid_cap,
+                        hipStream_t stream, int exp_flags) {
   if (batch == 0) return hipSuccess;
   const int grid = (int)(batch < grid_cap ? batch : grid_cap);
   const dim3 g(grid), blk(kFusedBlock);
-  if (i16 && wbf)
-    hipLaunchKernelGGL((wk_fused_kernel<int16_t, true>), g, blk, 0, stream, (const int16_t*)audio, batch, clip_stride,
-                       w, wbf, logits, feats_or_null, exp_flags);
-  else if (i16)
-    hipLaunchKernelGGL((wk_fused_kernel<int16_t, false>), g, blk, 0, stream, (const int16_t*)audio, batch, clip_stride,
-                       w, wbf, logits, feats_or_null, exp_flags);
-  else if (wbf)
-    hipLaunchKernelGGL((wk_fused_kernel<float, true>), g, blk, 0, stream, (const float*)audio, batch, clip_stride, w,
-                       wbf, logits, feats_or_null, exp_flags);
-  else
-    hipLaunchKernelGGL((wk_fused_kernel<float, false>), g, blk, 0, stream, (const float*)audio, batch, clip_stride, w,
-                       wbf, logits, feats_or_null, exp_flags);
+  if (conv_mode != kConvF32 && !wbf) return hipErrorInvalidValue;
+#define WK_FUSED_LAUNCH(T, CM)                                                                          \
+  hipLaunchKernelGGL((wk_fused_kernel<T, CM>), g, blk, 0, stream, (const T*)audio, batch, clip_stride, w, wbf, \
+                     logits, feats_or_null, exp_flags)
+  if (i16) {
+    if (conv_mode == kConvBf16) WK_FUSED_LAUNCH(int16_t, kConvBf16);
+    else if (conv_mode == kConvBf16x3) WK_FUSED_LAUNCH(int16_t, kConvBf16x3);
+    else WK_FUSED_LAUNCH(int16_t, kConvF32);
+  } else {
+    if (conv_mode == kConvBf16) WK_FUSED_LAUNCH(float, kConvBf16);
+    else if (conv_mode == kConvBf16x3) WK_FUSED_LAUNCH(float, kConvBf16x3);
+    else WK_FUSED_LAUNCH(float, kConvF32);
+  }
+#undef WK_FUSED_LAUNCH
   return hipGetLastError();
 }
 

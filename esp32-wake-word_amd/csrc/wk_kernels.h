@@ -42,9 +42,10 @@ hipError_t launch_cnn(const float* feats, int64_t batch, const float* w, float* 
 
 // Fused front-end + CNN (wk_fused.hip), mode B only.
 // w = fp32 fragment-major weights (pack_fragments); wbf = bf16 conv fragments
-// (pack_fragments_bf16) or null: non-null selects bf16 convolutions (config 4).
+// (pack_fragments_bf16; hi then lo parts for split bf16) for conv_mode 1
+// (bf16, config 4) and 2 (split bf16, WK_PREC_BF16X3); conv_mode 0 = fp32 MFMA.
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
-                        const uint16_t* wbf, float* logits, float* feats_or_null, int grid_cap, hipStream_t stream,
+                        const uint16_t* wbf, int conv_mode, float* logits, float* feats_or_null, int grid_cap, hipStream_t stream,
                         int exp_flags = 0);   // exp_flags (timing experiments only): 1 = FE role only, 2 = CNN only
 
 // int8 CNN in the device's esp-dl arithmetic (wk_int8.hip); feats [B][13][63] fp32.
@@ -96,7 +97,17 @@ inline uint16_t to_bf16_rne(float x) {
   return (uint16_t)(u >> 16);
 }
 
-inline void pack_fragments_bf16(const float* w, uint16_t* pk) {
+// lo = true packs the split-bf16 low parts, bf16(w - bf16(w)) (WK_PREC_BF16X3).
+inline uint16_t split_bf16(float x, bool lo) {
+  const uint16_t h = to_bf16_rne(x);
+  if (!lo) return h;
+  const uint32_t u = (uint32_t)h << 16;
+  float hf;
+  memcpy(&hf, &u, 4);
+  return to_bf16_rne(x - hf);
+}
+
+inline void pack_fragments_bf16(const float* w, uint16_t* pk, bool lo = false) {
   auto pack = [&](int off, int cout_tiles, int cin, int cin_pad, int wbase) {
     const int nsteps = 3 * cin_pad / 16;
     for (int t = 0; t < cout_tiles; ++t)
@@ -105,7 +116,7 @@ inline void pack_fragments_bf16(const float* w, uint16_t* pk) {
           for (int j = 0; j < 4; ++j) {
             const int co = 16 * t + (l & 15), k = 16 * s + 4 * (l >> 4) + j, tap = k / cin_pad, ci = k % cin_pad;
             pk[off + ((t * nsteps + s) * 64 + l) * 4 + j] =
-                ci < cin ? to_bf16_rne(w[wbase + (co * cin + ci) * 3 + tap]) : (uint16_t)0;
+                ci < cin ? split_bf16(w[wbase + (co * cin + ci) * 3 + tap], lo) : (uint16_t)0;
           }
   };
   pack(kPbW1, 2, 13, 16, kOffW1);

@@ -20,6 +20,7 @@ WK_DTYPE_I16 = 1
 WK_PREC_FP32 = 0
 WK_PREC_BF16 = 1
 WK_PREC_INT8 = 2
+WK_PREC_BF16X3 = 3
 WK_NUM_WEIGHTS = 40224
 
 # Every symbol include/wakeword.h declares (checked by tests/test_abi.py).

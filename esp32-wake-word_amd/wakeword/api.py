@@ -175,7 +175,8 @@ class KWSModel:
         self.device = device
         self.precision = precision
         self._h = _Handle(_lib.WK_MODE_TORCHAUDIO_CMVN, pack_weights(self._sd), device,
-                          {"fp32": _lib.WK_PREC_FP32, "bf16": _lib.WK_PREC_BF16, "int8": _lib.WK_PREC_INT8}[precision])
+                          {"fp32": _lib.WK_PREC_FP32, "bf16": _lib.WK_PREC_BF16, "int8": _lib.WK_PREC_INT8,
+                           "bf16x3": _lib.WK_PREC_BF16X3}[precision])
 
     # -- nn.Module-like surface ------------------------------------------------
     def state_dict(self) -> Dict[str, np.ndarray]:

@@ -44,11 +44,16 @@ typedef enum {
 } wk_mode;
 
 typedef enum { WK_DTYPE_F32 = 0, WK_DTYPE_I16 = 1 } wk_dtype;   /* audio sample type */
-/* CNN arithmetic.  INT8 = the device's esp-dl int8 network (power-of-2
- * per-tensor exponents of ml_models/xiaoa.info, round-half-even requant;
- * reproduces the xiaoa.info known-answer test exactly): a device-faithful
- * checking mode, run unfused after the fp32 front-end. */
-typedef enum { WK_PREC_FP32 = 0, WK_PREC_BF16 = 1, WK_PREC_INT8 = 2 } wk_precision;
+/* CNN arithmetic.  FP32 = fp32 MFMA.  BF16 = bf16 convolutions (SURVEY
+ * config 4), fp32 front-end/classifier.  INT8 = the device's esp-dl int8
+ * network (power-of-2 per-tensor exponents of ml_models/xiaoa.info,
+ * round-half-even requant; reproduces the xiaoa.info known-answer test
+ * exactly): a device-faithful checking mode, run unfused after the fp32
+ * front-end.  BF16X3 = fp32-grade convolutions on bf16 MFMA: activations and
+ * weights split into bf16 hi + lo parts, products hi*hi + hi*lo + lo*hi
+ * accumulated in fp32 (relative product error ~2^-16); same logit tolerance
+ * as FP32.  BF16 and BF16X3 run in the fused kernel (wk_forward) only. */
+typedef enum { WK_PREC_FP32 = 0, WK_PREC_BF16 = 1, WK_PREC_INT8 = 2, WK_PREC_BF16X3 = 3 } wk_precision;
 
 typedef struct {
   int32_t mode;            /* wk_mode                                               */

@@ -42,3 +42,51 @@ def test_bf16_cnn_only_entry_is_refused(m16):
     import wakeword
     with pytest.raises(wakeword.WakewordError, match="UNSUPPORTED"):
         m16(np.zeros((2, 13, 63), np.float32))
+
+
+# ---- WK_PREC_BF16X3: split-bf16 convolutions held to the fp32 logit tolerance.
+X3_LOGIT_ATOL = 1e-3   # the same bound as the fp32 path (tests/test_gpu_parity.py)
+
+
+@pytest.fixture(scope="module")
+def m3(gpu, golden_dir):
+    import wakeword
+    return wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"), precision="bf16x3")
+
+
+def test_bf16x3_golden_wavs(m3, golden_dir):
+    w = np.load(os.path.join(golden_dir, "wavs.npz"))
+    got = m3.detect(w["x_noise"]).reshape(-1).cpu().numpy()
+    ref = w["logit_noise"].reshape(-1)
+    assert np.abs(got - ref).max() <= X3_LOGIT_ATOL
+
+
+@pytest.mark.parametrize("n", [1, 5, 300])
+def test_bf16x3_synth_vs_oracle(m3, xiaoa_sd, n):
+    x = O.synth_clips(41, 0, n, 16000)
+    got = m3.detect(x).reshape(-1).cpu().numpy()
+    ref = O.detect_mode_b(x[: min(n, 32)].astype(np.float64), xiaoa_sd)
+    assert np.abs(got[: ref.size] - ref).max() <= X3_LOGIT_ATOL
+    one = m3.detect(x[:1]).reshape(-1).cpu().numpy()
+    np.testing.assert_array_equal(one, got[:1])
+
+
+def test_bf16x3_tracks_fp32_at_scale(m3, golden_dir):
+    """65,536 device-generated clips: split-bf16 against the fp32-MFMA path, clip for clip."""
+    import torch
+    import wakeword
+    m32 = wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"))
+    x = wakeword.synth_clips(1234, 0, 65536, device=0)
+    a = m3.detect(x).reshape(-1)
+    b = m32.detect(x).reshape(-1)
+    d = (a - b).abs().max().item()
+    assert d <= X3_LOGIT_ATOL, d
+    assert bool(torch.isfinite(a).all())
+
+
+def test_bf16x3_int16_matches_float(m3):
+    x = O.synth_clips(43, 0, 7, 16000)
+    q = np.round(x * 32767).astype(np.int16)
+    a = m3.detect(q).reshape(-1).cpu().numpy()
+    b = m3.detect(q.astype(np.float32) / 32768.0).reshape(-1).cpu().numpy()
+    np.testing.assert_allclose(a, b, atol=1e-5)
