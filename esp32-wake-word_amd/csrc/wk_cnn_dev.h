@@ -121,12 +121,15 @@ __device__ __forceinline__ void epi_pool_bf(const f32x4& acc, uint16_t* __restri
 // product is exact in the fp32 accumulator, so the per-product error is
 // ~2^-16 relative -- three v_mfma_f32_16x16x16_bf16 (8 passes each) in place
 // of four v_mfma_f32_16x16x4f32 (fp32 MFMA: 1/16 the bf16 rate).  Images hold
-// xh at ci and xl at ci + LO (LO = 16 CB) of the same t row; the cross terms
-// go to separate accumulators (summed by the caller) to space dependent MFMAs.
+// xh at ci and xl at ci + LO (LO = 16 CB) of the same t row.  All three
+// products chain on one accumulator per tile (D tied to SrcC): with separate
+// cross-term accumulators the compiler placed MFMA destinations over other
+// MFMAs' live B/SrcC registers and the results were not reproducible
+// (1 clip in ~65k differed run to run).
 template <int NSTEP, int CB, int CIP, int CHUNK = 0>
 __device__ __forceinline__ void conv_pair_bf3(const uint16_t* __restrict__ img, const s4 (&wh)[NSTEP],
                                               const s4 (&wl)[NSTEP], int boff_a, int boff_b, f32x4& acc_a,
-                                              f32x4& acc_b, f32x4& x_a, f32x4& x_b) {
+                                              f32x4& acc_b) {
   constexpr int LO = 16 * CB;
 #pragma unroll
   for (int s = 0; s < NSTEP; ++s) {
@@ -135,12 +138,12 @@ __device__ __forceinline__ void conv_pair_bf3(const uint16_t* __restrict__ img, 
     const s4 hb = *reinterpret_cast<const s4*>(img + boff_b + off);
     const s4 la = *reinterpret_cast<const s4*>(img + boff_a + off + LO);
     const s4 lb = *reinterpret_cast<const s4*>(img + boff_b + off + LO);
+    acc_a = mfma_bf16(wl[s], ha, acc_a);
+    acc_b = mfma_bf16(wl[s], hb, acc_b);
+    acc_a = mfma_bf16(wh[s], la, acc_a);
+    acc_b = mfma_bf16(wh[s], lb, acc_b);
     acc_a = mfma_bf16(wh[s], ha, acc_a);
     acc_b = mfma_bf16(wh[s], hb, acc_b);
-    x_a = mfma_bf16(wl[s], ha, x_a);
-    x_b = mfma_bf16(wl[s], hb, x_b);
-    x_a = mfma_bf16(wh[s], la, x_a);
-    x_b = mfma_bf16(wh[s], lb, x_b);
     if (CHUNK > 0 && (s % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
   }
 }

@@ -49,6 +49,22 @@ template <> __device__ __forceinline__ int16_t raw_ld<int16_t>(__amdgpu_buffer_r
   return (int16_t)__builtin_amdgcn_raw_buffer_load_b16(r, idx * 2, 0, 0);
 }
 
+// The adjacent pair x[idx], x[idx + 1] as one 8-byte (fp32) / 4-byte (int16)
+// load: half the load instructions of two raw_ld (the front-end's loads are
+// issue-bound: 8 front-end waves per CU share one load path).
+template <typename T> __device__ __forceinline__ void raw_ld2(__amdgpu_buffer_rsrc_t r, int idx, T& a, T& b);
+template <> __device__ __forceinline__ void raw_ld2<float>(__amdgpu_buffer_rsrc_t r, int idx, float& a, float& b) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, idx * 4, 0, 0);
+  a = __uint_as_float(v[0]);   // (not __builtin_bit_cast of a vector element: miscompiled to v[0] for both)
+  b = __uint_as_float(v[1]);
+}
+template <> __device__ __forceinline__ void raw_ld2<int16_t>(__amdgpu_buffer_rsrc_t r, int idx, int16_t& a,
+                                                            int16_t& b) {
+  const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(r, idx * 2, 0, 0);
+  a = (int16_t)(v & 0xFFFFu);
+  b = (int16_t)(v >> 16);
+}
+
 // Reflect index i of the centred (padded) signal of length n into [0, n).
 __device__ __forceinline__ int refl_idx(int i, int n) {
   i = i < 0 ? -i : i;
@@ -64,10 +80,7 @@ __device__ __forceinline__ void load_raw(__amdgpu_buffer_rsrc_t rs, int base, in
   if (!general) {
     const int v0 = base + 2 * j;
 #pragma unroll
-    for (int n1 = 0; n1 < 10; ++n1) {
-      r.x0[n1] = raw_ld<T>(rs, v0 + 32 * n1);
-      r.x1[n1] = raw_ld<T>(rs, v0 + 32 * n1 + 1);
-    }
+    for (int n1 = 0; n1 < 10; ++n1) raw_ld2<T>(rs, v0 + 32 * n1, r.x0[n1], r.x1[n1]);
     r.xb = raw_ld<T>(rs, base - 1);   // mode A frame 0: index -1 -> 0 (y[0] = x[0], mfcc.c:70)
   } else {
 #pragma unroll

@@ -331,10 +331,9 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
           epi_pool_bf<I1_CIP, I1_TP, 31>(acc_b, B1, co0, cl, tb, lane);
         } else if constexpr (X3) {
           const int bx = (cl * I0_TP + li) * X0_CIP + 4 * lk;
-          f32x4 x_a = {0, 0, 0, 0}, x_b = {0, 0, 0, 0};
-          conv_pair_bf3<3, 1, X0_CIP>(X0, w1b, w1l, bx + ta * X0_CIP, bx + tb * X0_CIP, acc_a, acc_b, x_a, x_b);
-          epi_pool_bf3<X1_CIP, I1_TP, 31, 32>(acc_a + x_a, X1, co0, cl, ta, lane);
-          epi_pool_bf3<X1_CIP, I1_TP, 31, 32>(acc_b + x_b, X1, co0, cl, tb, lane);
+          conv_pair_bf3<3, 1, X0_CIP>(X0, w1b, w1l, bx + ta * X0_CIP, bx + tb * X0_CIP, acc_a, acc_b);
+          epi_pool_bf3<X1_CIP, I1_TP, 31, 32>(acc_a, X1, co0, cl, ta, lane);
+          epi_pool_bf3<X1_CIP, I1_TP, 31, 32>(acc_b, X1, co0, cl, tb, lane);
         } else {
           conv_pair_v<1, I0_CIP, 1>(F0, w1, bo + ta * I0_CIP, bo + tb * I0_CIP, acc_a, acc_b);
           epi_pool_v<I1_CIP, I1_TP, 31>(acc_a, F1, co0, cl, ta, lane);
@@ -372,10 +371,10 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
         const int bb = (cl * I1_TP + li) * X1_CIP + 4 * lk;
-        f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0}, x_a = {0, 0, 0, 0}, x_b = {0, 0, 0, 0};
-        conv_pair_bf3<6, 2, X1_CIP>(X1, w2b, w2l, bb, bb + 16 * X1_CIP, acc_a, acc_b, x_a, x_b);
-        epi_pool_bf3<X2_CIP, I2_TP, 15, 64>(acc_a + x_a, X2, co0, cl, 0, lane);
-        epi_pool_bf3<X2_CIP, I2_TP, 15, 64>(acc_b + x_b, X2, co0, cl, 16, lane);
+        f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
+        conv_pair_bf3<6, 2, X1_CIP>(X1, w2b, w2l, bb, bb + 16 * X1_CIP, acc_a, acc_b);
+        epi_pool_bf3<X2_CIP, I2_TP, 15, 64>(acc_a, X2, co0, cl, 0, lane);
+        epi_pool_bf3<X2_CIP, I2_TP, 15, 64>(acc_b, X2, co0, cl, 16, lane);
       }
     } else {
       float w2[24];
@@ -411,11 +410,8 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 #pragma unroll
           for (int s = 0; s < 12; ++s) w3l[s] = frag_bf(kLoW + kPbW3 + (cw * 12 + s) * 256);
           const int bx = li * X2_CIP + 4 * lk;
-          f32x4 x_a = {0, 0, 0, 0}, x_b = {0, 0, 0, 0};
           conv_pair_bf3<12, 4, X2_CIP, 3>(X2, w3b, w3l, bx + ca * I2_TP * X2_CIP, bx + cb * I2_TP * X2_CIP, acc_a,
-                                          acc_b, x_a, x_b);
-          acc_a += x_a;
-          acc_b += x_b;
+                                          acc_b);
         } else {
           conv_pair_v<4, I2_CIP, 2>(F2, w3, bo + ca * I2_TP * I2_CIP, bo + cb * I2_TP * I2_CIP, acc_a, acc_b);
         }

@@ -90,3 +90,16 @@ def test_bf16x3_int16_matches_float(m3):
     a = m3.detect(q).reshape(-1).cpu().numpy()
     b = m3.detect(q.astype(np.float32) / 32768.0).reshape(-1).cpu().numpy()
     np.testing.assert_allclose(a, b, atol=1e-5)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16x3"])
+def test_fused_repeatable_at_scale(gpu, golden_dir, precision):
+    """Four full-size launches (65,536 clips) give bit-identical logits: the
+    fused kernel's role hand-offs and MFMA chains have no timing dependence."""
+    import wakeword
+    m = wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"), precision=precision)
+    x = wakeword.synth_clips(777, 0, 65536, device=0)
+    ref = m.detect(x).reshape(-1)
+    for _ in range(4):
+        got = m.detect(x).reshape(-1)
+        assert int((got != ref).sum()) == 0

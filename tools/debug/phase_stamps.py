@@ -14,8 +14,9 @@ from wakeword import _lib  # noqa: E402
 
 L = _lib.lib()
 L.wk_debug_stamps.argtypes = [C.c_void_p, C.c_int]
-model = wakeword.load_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"))
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+prec = sys.argv[2] if len(sys.argv) > 2 else "fp32"
+model = wakeword.load_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"), precision=prec)
 x = wakeword.synth_clips(1234, 0, B)
 model.detect(x)
 torch.cuda.synchronize()
@@ -28,10 +29,10 @@ torch.cuda.synchronize()
 L.wk_debug_stamps(buf.ctypes.data, 1)
 grid = min(B, 256)
 clips_per_wg = B / grid
-fe = ["stage0", "pf_issue", "dft1", "tw+trW", "trR", "dft2", "split", "sync1", "mel", "sync2", "act0",
-      "dct+out"]
-cnn = ["wait_feat", "conv1", "sync1", "conv2", "sync2", "conv3", "sync3", "fc1+sync", "fc2"]
-print(f"cycles per clip per wave (B={B}, grid={grid}, reps={reps})")
+# stamp ids: wk_fused.hip fe_role (0, 1, 7-10) and wk_fe_dev.h fe_rest (2-6); cnn_role 0-8
+fe = ["stage0", "pf_issue", "dft1", "tw+trW", "trR", "dft2", "split", "sync_P", "mel", "p_wait", "L_free", "-"]
+cnn = ["dct+waitL", "conv1", "sync1", "conv2", "sync2", "conv3", "sync3", "fc1+sync", "fc2"]
+print(f"cycles per clip per wave (B={B}, grid={grid}, reps={reps}, precision={prec})")
 for w in range(8):
     row = buf[w, :12].astype(np.float64) / (grid * reps * clips_per_wg)
     print(f"FE  w{w}: " + " ".join(f"{n}={v:5.0f}" for n, v in zip(fe, row)) + f"  total={row.sum():6.0f}")
