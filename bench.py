@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--audio", default="f32", choices=["f32", "i16"],
+                    help="sample type of the resident clips: f32 (the metric's workload, 64,000 B/window) or "
+                         "i16 PCM (32,000 B/window, scaled by 1/32768 on load)")
     ap.add_argument("--precision", default="fp32", choices=list(PRECISIONS),
                     help="CNN convolutions: fp32 MFMA (config 2, default), bf16 (config 4), or bf16x3 "
                          "(config 2 at fp32-grade accuracy on split-bf16 MFMA); front-end fp32 always")
@@ -123,6 +126,10 @@ def main():
                                precision=args.precision)
     first, count = weak_shard(B, rank)                     # per-rank clip split, no collective
     clips = wakeword.synth_clips(args.seed, first, count, 16000, device=local)   # resident in HBM
+    adt = _lib.WK_DTYPE_F32
+    if args.audio == "i16":
+        clips = (clips * 32768.0).round().clamp(-32768, 32767).to(torch.int16)
+        adt = _lib.WK_DTYPE_I16
     logits = torch.empty((B,), dtype=torch.float32, device=f"cuda:{local}")
     L = _lib.lib()
     h = model._h.h
@@ -131,7 +138,7 @@ def main():
     aptr, lptr = C.c_void_p(clips.data_ptr()), C.c_void_p(logits.data_ptr())
 
     def step():
-        st = L.wk_forward(h, aptr, _lib.WK_DTYPE_F32, B, 16000, 16000, lptr, None, sptr)
+        st = L.wk_forward(h, aptr, adt, B, 16000, 16000, lptr, None, sptr)
         if st != 0:
             _lib.check(st, "wk_forward")
 
@@ -178,6 +185,7 @@ def main():
             "data": "synthetic: device counter-hash generator, clamp(0.1*N(0,1))+440 Hz sine on odd clips "
                     "(SURVEY 8(d) config 2); xiaoa.onnx weights",
             "config": {"workload": PRECISIONS[args.precision][1],
+                       "audio": "fp32 samples" if args.audio == "f32" else "int16 PCM samples",
                        "batch_per_gpu": B, "global_batch": world * B, "seq_len": 16000,
                        "parallelism": f"dp{world} (per-rank clip split, no collectives)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
@@ -185,7 +193,8 @@ def main():
                          "traffic": (traffic_bpw * B if traffic_bpw else None),
                          "launch_ms": round(launch_ms, 4),
                          "flop_per_window": FLOP_PER_WINDOW,
-                         "hbm_gbs_algorithmic": round(BYTES_PER_WINDOW_F32 * B / (launch_ms * 1e-3) / 1e9, 1)},
+                         "hbm_gbs_algorithmic": round((BYTES_PER_WINDOW_F32 if args.audio == "f32" else 32_004) * B
+                                                      / (launch_ms * 1e-3) / 1e9, 1)},
             "logits_finite": finite,
         }
         if traffic_src:

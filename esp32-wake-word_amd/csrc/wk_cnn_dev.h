@@ -122,10 +122,9 @@ __device__ __forceinline__ void epi_pool_bf(const f32x4& acc, uint16_t* __restri
 // ~2^-16 relative -- three v_mfma_f32_16x16x16_bf16 (8 passes each) in place
 // of four v_mfma_f32_16x16x4f32 (fp32 MFMA: 1/16 the bf16 rate).  Images hold
 // xh at ci and xl at ci + LO (LO = 16 CB) of the same t row.  All three
-// products chain on one accumulator per tile (D tied to SrcC): with separate
-// cross-term accumulators the compiler placed MFMA destinations over other
-// MFMAs' live B/SrcC registers and the results were not reproducible
-// (1 clip in ~65k differed run to run).
+// products chain on one accumulator per tile (no VALU sum of partial
+// accumulators in the epilogue; measured faster than separate cross-term
+// accumulators).
 template <int NSTEP, int CB, int CIP, int CHUNK = 0>
 __device__ __forceinline__ void conv_pair_bf3(const uint16_t* __restrict__ img, const s4 (&wh)[NSTEP],
                                               const s4 (&wl)[NSTEP], int boff_a, int boff_b, f32x4& acc_a,

@@ -189,9 +189,12 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
   //   U = 2 X[k] = S - i bb,  U' = conj(2 X[256-k]) = S + i bb
   // (mode B folds the 1/4 of |X|^2 = |U|^2/4 into the filterbank weights).
   // {|U|^2, |U'|^2} is one packed pair: {Ux, U'x}^2 + {Uy, U'y}^2.
-  // Partner: lane (16-j)&15 of this group, register 15-k2 (ds_bpermute);
+  // Partner: lane (16-j)&15 of this group, register 15-k2, fetched by two DPP
+  // row moves (row_mirror: j <- 15-j, then row_ror:1: j <- j-1), no LDS trip;
   // lane 0 holds its own partner in register (16-k2)&15.
+#ifdef WK_SPLIT_BPERMUTE
   const int src = ((lane & 48) | ((16 - j) & 15)) << 2;
+#endif
   f2 sc0 = {1.0f, 1.0f}, sc = {1.0f, 1.0f};
   if constexpr (!MODE_B) {
     // mfcc.c:267 power = |X|^2 / n_fft + 1e-12 = |U|^2 / 2048 + 1e-12; the
@@ -208,8 +211,13 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
     if (k2 < 8) {
       const f2 s = c[dft16_out(15 - k2)];
       const f2 own = c[dft16_out((16 - k2) & 15)];
+#ifdef WK_SPLIT_BPERMUTE
       const float pr = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.x)));
       const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.y)));
+#else
+      const float pr = dpp<0x121>(dpp<0x140>(s.x));
+      const float pi = dpp<0x121>(dpp<0x140>(s.y));
+#endif
       zq = j == 0 ? own : f2{pr, pi};
     } else {
       zq = c[dft16_out(8)];

@@ -79,7 +79,15 @@ enum { kConvF32 = 0, kConvBf16 = 1, kConvBf16x3 = 2 };
 constexpr int kFusedLds = kImgEnd;
 static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 
-enum { kCtrlFeBar = 0, kCtrlCnnBar = 1, kCtrlLReady = 2, kCtrlLFree = 3, kCtrlAbort = 15 };
+// kCtrlLFree + w (w = CNN wave 0..7): clips whose log-mel buffer CNN wave w
+// has finished reading.  Per wave, not one shared count: the CNN waves are not
+// lock-stepped inside a batch's DCT loop (and the classifier.2 wave starts the
+// next batch late), so a summed count can reach 8 (i - 1) while one wave is
+// still reading clip i - 2's buffer -- 7 waves ahead by a clip or more paid
+// for the laggard.  That race corrupted the laggard's DCT coefficients in ~1
+// clip per 65k (seen with split-bf16 timing).  The other counters are sound as
+// sums: their producers pass a barrier between consecutive signals.
+enum { kCtrlFeBar = 0, kCtrlCnnBar = 1, kCtrlLReady = 2, kCtrlLFree = 4, kCtrlAbort = 15 };
 // Every spin is bounded (~4M sleeps, well under a second): a protocol bug
 // yields wrong logits and a drained grid, never a hung GPU.
 constexpr unsigned kSpinLimit = 1u << 22;
@@ -112,6 +120,32 @@ __device__ __forceinline__ void role_sync(unsigned* ctrl, int idx, unsigned& gen
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(ctrl + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   spin_until(ctrl, idx, gen);
+}
+
+// Spin until ctrl[idx + w] >= v for all w < 8 (same abort rules as spin_until).
+__device__ __forceinline__ void spin_until_all8(unsigned* ctrl, int idx, unsigned v) {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  for (unsigned n = 0;; ++n) {
+    unsigned m = lds_load(ctrl + idx);
+#pragma unroll
+    for (int w = 1; w < 8; ++w) m = min(m, lds_load(ctrl + idx + w));
+    if (m >= v) break;
+    if (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort)) {
+      __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// Publish a per-wave progress value once this wave's LDS ops are complete.
+__device__ __forceinline__ void signal_set(unsigned* ctrl, int idx, unsigned v, int lane) {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_store(ctrl + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
 __device__ __forceinline__ void signal_add(unsigned* ctrl, int idx, int lane) {
@@ -167,6 +201,10 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
         if ((wave >= 4) == (r == 1)) __builtin_amdgcn_s_setprio(1); else __builtin_amdgcn_s_setprio(0);
       }
       f2 a[16];
+#ifdef WK_STAMPS
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: time the wait for the prefetched audio apart
+      WK_STAMP(11);
+#endif
       if (fl < kNFramesB) fe_stage0<true>(pf, 256 * fl - 160, kWinSamples, j, general, tb, a);
       WK_STAMP(0);
       prefetch(r == 0 ? i : i + 1, r ^ 1, pf);
@@ -180,7 +218,7 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
     if (exp_flags & 4) __builtin_amdgcn_s_setprio(1); else if (exp_flags & 8) __builtin_amdgcn_s_setprio(0);
     role_sync(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
     WK_STAMP(7);
-    if (i >= 2 && !(exp_flags & 1)) spin_until(ctrl, kCtrlLFree, 8u * (unsigned)(i - 1));   // clip i-2's DCT done
+    if (i >= 2 && !(exp_flags & 1)) spin_until_all8(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
     WK_STAMP(10);
     mel_dispatch<true>(wave, P + min(lane, kNFramesB - 1) * kPRow, (i & 1 ? L1 : L) + lane);
     WK_STAMP(8);
@@ -311,7 +349,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
             if (fo) fo[c0 * kNFramesB] = y;
           }
         }
-        signal_add(ctrl, kCtrlLFree, lane);   // this wave's reads of the log-mel buffer are done
+        signal_set(ctrl, kCtrlLFree + cw, (unsigned)(i + 1), lane);   // this wave's reads of the log-mel buffer are done
       }
     }
     WK_STAMP(0);
@@ -446,7 +484,10 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     WK_STAMP(7);
 
     // ReLU -> classifier.2 (64 -> 1): lane = (o group q = lane>>2, clip = lane&3).
-    if (cw == 0) {
+#ifndef WK_FC2_WAVE
+#define WK_FC2_WAVE 0
+#endif
+    if (cw == WK_FC2_WAVE) {
       int ln = lane;
       asm volatile("" : "+v"(ln));
       const int cl = ln & (NBF - 1), q = ln >> 2;
@@ -465,6 +506,9 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
       if (q == 0 && i < n_mine) logits[(int64_t)blockIdx.x + G * i] = acc;
     }
     WK_STAMP(8);
+#ifdef WK_SYNC_AFTER_FC2
+    role_sync(ctrl, kCtrlCnnBar, gen, lane);
+#endif
   }
   WK_STAMP_FLUSH(8 + cw);
 }

@@ -30,7 +30,7 @@ L.wk_debug_stamps(buf.ctypes.data, 1)
 grid = min(B, 256)
 clips_per_wg = B / grid
 # stamp ids: wk_fused.hip fe_role (0, 1, 7-10) and wk_fe_dev.h fe_rest (2-6); cnn_role 0-8
-fe = ["stage0", "pf_issue", "dft1", "tw+trW", "trR", "dft2", "split", "sync_P", "mel", "p_wait", "L_free", "-"]
+fe = ["stage0", "pf_issue", "dft1", "tw+trW", "trR", "dft2", "split", "sync_P", "mel", "p_wait", "L_free", "vm_wait"]
 cnn = ["dct+waitL", "conv1", "sync1", "conv2", "sync2", "conv3", "sync3", "fc1+sync", "fc2"]
 print(f"cycles per clip per wave (B={B}, grid={grid}, reps={reps}, precision={prec})")
 for w in range(8):
