@@ -5,6 +5,9 @@
 #include "wk_common.h"
 #include "wk_tables.h"
 
+#ifndef WK_SPLIT_G
+#define WK_SPLIT_G 3   // real-FFT split chains interleaved per group (fe_rest)
+#endif
 #ifndef WK_TW_GROUP
 #define WK_TW_GROUP 0   // >0: fence the twiddle LDS reads into groups of this many (0 = compiler schedules; measured equal)
 #endif
@@ -94,6 +97,29 @@ __device__ __forceinline__ void load_raw(__amdgpu_buffer_rsrc_t rs, int base, in
   }
 }
 
+// Part k (0..3) of load_raw: rows n1 in [3k, 3k+3) (and xb with part 0), so
+// a round's prefetch can be spread over the round instead of issued as one
+// burst (eight waves issuing 11 loads each at once filled the TA FIFOs and
+// stalled issue).  The edge-frame (GENERAL) form is issued whole with part 0.
+template <bool MODE_B, typename T>
+__device__ __forceinline__ void load_raw_part(__amdgpu_buffer_rsrc_t rs, int base, int j, int n, bool act,
+                                              bool general, Raw<T>& r, int part) {
+  if (!act) return;
+  if (general) {
+    if (part == 0) load_raw<MODE_B, T>(rs, base, j, n, act, true, r);
+    return;
+  }
+  const int v0 = base + 2 * j;
+#pragma unroll
+  for (int n1 = 0; n1 < 10; ++n1)
+    if (n1 / 3 == part) raw_ld2<T>(rs, v0 + 32 * n1, r.x0[n1], r.x1[n1]);
+  if (part == 0) r.xb = raw_ld<T>(rs, base - 1);
+}
+
+struct NoPrefetch {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
 __device__ __forceinline__ float row_ror1(float v) {  // lane l <- lane (l-1) mod 16 of its 16-lane row
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xF, 0xF, false));
 }
@@ -115,7 +141,14 @@ struct FeTables {
 template <bool MODE_B, typename T>
 __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, int j, bool general,
                                           const FeTables& tb, f2 (&a)[16], float pre = -0.97f WK_SP_PARAM) {
+  // All ten window pairs are read up front: issued one per iteration they
+  // each exposed a full LDS round trip (the edge-frame branch kept the
+  // compiler from hoisting them).
+  f2 w[10];
+#pragma unroll
+  for (int n1 = 0; n1 < 10; ++n1) w[n1] = *reinterpret_cast<const f2*>(tb.win + 32 * n1 + 2 * j);
   float prev_rot = 0.0f;
+  float y0[10], y1[10];
 #pragma unroll
   for (int n1 = 0; n1 < 10; ++n1) {
     const float x0 = to_f(raw.x0[n1]), x1 = to_f(raw.x1[n1]);
@@ -126,9 +159,13 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
     asm volatile("" : "+v"(rot));
     const float xm = j != 0 ? rot : (n1 == 0 ? to_f(raw.xb) : prev_rot);
     prev_rot = rot;
-    float y0 = __builtin_fmaf(pre, xm, x0);   // pre = -0.97 (0 for mfcc.c's single-frame variant)
-    float y1 = __builtin_fmaf(pre, x0, x1);
-    if (MODE_B && general) {
+    y0[n1] = __builtin_fmaf(pre, xm, x0);   // pre = -0.97 (0 for mfcc.c's single-frame variant)
+    y1[n1] = __builtin_fmaf(pre, x0, x1);
+  }
+  if (MODE_B && general) {   // wave-uniform: the two reflected edge frames only
+#pragma unroll
+    for (int n1 = 0; n1 < 10; ++n1) {
+      const float x0 = to_f(raw.x0[n1]), x1 = to_f(raw.x1[n1]);
       const int i0 = base + 32 * n1 + 2 * j;
       float nx = row_rol1(x0);
       float nx1 = row_rol1(to_f(raw.x0[n1 + 1 < 10 ? n1 + 1 : 9]));
@@ -136,22 +173,26 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
       const float xn = j != 15 ? nx : (n1 < 9 ? nx1 : to_f(raw.xb));
       const bool reflected = i0 < 0 || i0 > n - 1;
       const float r0 = __builtin_fmaf(pre, x1, x0), r1 = __builtin_fmaf(pre, xn, x1);
-      y0 = reflected ? r0 : (i0 == 0 ? x0 : y0);
-      y1 = reflected ? r1 : y1;
+      y0[n1] = reflected ? r0 : (i0 == 0 ? x0 : y0[n1]);
+      y1[n1] = reflected ? r1 : y1[n1];
     }
-    const f2 w = *reinterpret_cast<const f2*>(tb.win + 32 * n1 + 2 * j);
-    a[n1] = f2{y0, y1} * w;
   }
+#pragma unroll
+  for (int n1 = 0; n1 < 10; ++n1) a[n1] = f2{y0[n1], y1[n1]} * w[n1];
 #pragma unroll
   for (int n1 = 10; n1 < 16; ++n1) a[n1] = f2{0.0f, 0.0f};
 }
 
 // Stages 1..4 of one frame -> its power row (bins 0..256) in LDS.  All
 // complex arithmetic is packed fp32 (see f2 in wk_common.h).
-template <bool MODE_B>
+// pf(k), k = 0..3, is called at four points of the round (prefetch parts).
+template <bool MODE_B, typename PF = NoPrefetch>
 __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __restrict__ row, const FeTables& tb,
-                                        f2 w512, int esp_pack WK_SP_PARAM) {
+                                        f2 w512, int esp_pack, const PF& pf = PF() WK_SP_PARAM) {
+  pf(0);
+#ifndef WK_ABL_NODFT   // WK_ABL_*: timing ablations of tools/debug (wrong results)
   dft16(a);  // A[k1] at a[dft16_out(k1)]
+#endif
   WK_FE_HIT(2);
 
   // twiddle W256^(j*k1) + 16x16 transpose through this frame's LDS row (pitch 17).
@@ -162,13 +203,22 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
   row[j] = b[0].x;
 #pragma unroll
   for (int k1 = 1; k1 < 16; ++k1) {
+#ifdef WK_ABL_NOTW
+    const f2 w = f2{0.5f, 0.25f};
+#else
     const f2 w = *reinterpret_cast<const f2*>(tb.tw + ((k1 - 1) * 16 + j) * 2);
+#endif
     b[k1] = cmul2(a[dft16_out(k1)], w);
     row[17 * k1 + j] = b[k1].x;
     if (WK_TW_GROUP > 0 && (k1 % (WK_TW_GROUP > 0 ? WK_TW_GROUP : 1)) == WK_TW_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
   }
   WK_FE_HIT(3);
+  pf(1);
   f2 c[16];
+#ifdef WK_ABL_NOTRANS
+#pragma unroll
+  for (int n2 = 0; n2 < 16; ++n2) c[n2] = b[n2];
+#else
   wave_lds_sync();
 #pragma unroll
   for (int n2 = 0; n2 < 16; ++n2) c[n2].x = row[17 * j + n2];
@@ -179,9 +229,14 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
 #pragma unroll
   for (int n2 = 0; n2 < 16; ++n2) c[n2].y = row[17 * j + n2];
   wave_lds_sync();
+#endif
   WK_FE_HIT(4);
 
+  pf(2);
+#ifndef WK_ABL_NODFT
   dft16(c);  // Z[j + 16*k2] at c[dft16_out(k2)]
+#endif
+  pf(3);
   WK_FE_HIT(5);
 
   // Real-FFT split, k = j + 16*k2 (k2 = 0..8), with the partner Z[256 - k]:
@@ -204,41 +259,69 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
     sc = f2{e, e};
     sc0 = esp_pack ? (j == 0 ? f2{1.0f / 2048.0f, 0.0f} : sc) : sc;  // j==0, k2==0: bins 0 and 256
   }
-#pragma unroll
-  for (int k2 = 0; k2 <= 8; ++k2) {
-    const f2 zk = c[dft16_out(k2)];
-    f2 zq;
-    if (k2 < 8) {
-      const f2 s = c[dft16_out(15 - k2)];
-      const f2 own = c[dft16_out((16 - k2) & 15)];
-#ifdef WK_SPLIT_BPERMUTE
-      const float pr = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.x)));
-      const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(s.y)));
-#else
-      const float pr = dpp<0x121>(dpp<0x140>(s.x));
-      const float pi = dpp<0x121>(dpp<0x140>(s.y));
+  // The nine k2 chains are ~20 dependent packed ops each; run them WK_SPLIT_G
+  // at a time, stage by stage, so independent ops fill each other's latency
+  // (left to itself the scheduler emitted them back to back, one chain at a
+  // time, with s_nop between dependent v_pk ops).
+#ifdef WK_ABL_NOSPLIT
+  row[j] = c[0].x + c[1].y + c[5].x + c[9].y + c[13].x;
+  return;
 #endif
-      zq = j == 0 ? own : f2{pr, pi};
-    } else {
-      zq = c[dft16_out(8)];
+  constexpr int G = WK_SPLIT_G;
+#pragma unroll
+  for (int k0 = 0; k0 <= 8; k0 += G) {
+    f2 S[G], D[G], pw[G];
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const int k2 = k0 + t;
+      if (k2 > 8) continue;
+      const f2 zk = c[dft16_out(k2)];
+      f2 zq;
+      if (k2 < 8) {
+        const f2 sv = c[dft16_out(15 - k2)];
+        const f2 own = c[dft16_out((16 - k2) & 15)];
+#ifdef WK_SPLIT_BPERMUTE
+        const float pr = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sv.x)));
+        const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sv.y)));
+#else
+        const float pr = dpp<0x121>(dpp<0x140>(sv.x));
+        const float pi = dpp<0x121>(dpp<0x140>(sv.y));
+#endif
+        zq = j == 0 ? own : f2{pr, pi};
+      } else {
+        zq = c[dft16_out(8)];
+      }
+      S[t] = fma2(zq, f2{1.0f, -1.0f}, zk);
+      D[t] = fma2(zq, f2{-1.0f, 1.0f}, zk);
     }
-    const f2 S = fma2(zq, f2{1.0f, -1.0f}, zk);
-    const f2 D = fma2(zq, f2{-1.0f, 1.0f}, zk);
-    f2 Dw;
-    if (k2 == 0) Dw = D;
-    else if (k2 == 8) Dw = swp(D) * f2{1.0f, -1.0f};   // W32^8 = -i
-    else Dw = cmulc(D, w32(k2));
-    const f2 bb = cmul2(Dw, w512);
-    const f2 uvx = fma2(by(bb), f2{1.0f, -1.0f}, bx(S));
-    const f2 uvy = fma2(bx(bb), f2{-1.0f, 1.0f}, by(S));
-    f2 pw = fma2(uvx, uvx, uvy * uvy);
-    if constexpr (!MODE_B) pw = fma2(pw, k2 == 0 ? sc0 : sc, f2{1e-12f, 1e-12f});
-    const int kb = j + 16 * k2;
-    if (k2 < 8) {
-      row[kb] = pw.x;
-      row[256 - kb] = pw.y;
-    } else if (j == 0) {
-      row[128] = pw.x;
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const int k2 = k0 + t;
+      if (k2 > 8) continue;
+      if (k2 == 8) D[t] = swp(D[t]) * f2{1.0f, -1.0f};   // W32^8 = -i
+      else if (k2 > 0) D[t] = cmulc(D[t], w32(k2));
+    }
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const int k2 = k0 + t;
+      if (k2 > 8) continue;
+      const f2 bb = cmul2(D[t], w512);
+      const f2 uvx = fma2(by(bb), f2{1.0f, -1.0f}, bx(S[t]));
+      const f2 uvy = fma2(bx(bb), f2{-1.0f, 1.0f}, by(S[t]));
+      pw[t] = fma2(uvx, uvx, uvy * uvy);
+      if constexpr (!MODE_B) pw[t] = fma2(pw[t], k2 == 0 ? sc0 : sc, f2{1e-12f, 1e-12f});
+    }
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const int k2 = k0 + t;
+      if (k2 > 8) continue;
+      const int kb = j + 16 * k2;
+      if (k2 < 8) {
+        row[kb] = pw[t].x;
+        row[256 - kb] = pw[t].y;
+      } else if (j == 0) {
+        row[128] = pw[t].x;
+      }
     }
   }
   WK_FE_HIT(6);

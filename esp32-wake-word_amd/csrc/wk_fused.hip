@@ -76,7 +76,10 @@ static_assert(kX2Off + NBF * I2_TP * X2_CIP / 2 <= kImgEnd, "split images fit th
 static_assert(kF1Off % 4 == 0 && kF2Off % 4 == 0 && kB1Off % 2 == 0 && kB2Off % 2 == 0 && kX1Off % 2 == 0 &&
                   kX2Off % 2 == 0, "vector-aligned images");
 enum { kConvF32 = 0, kConvBf16 = 1, kConvBf16x3 = 2 };
-constexpr int kFusedLds = kImgEnd;
+// Scratch power row for the one frame slot past the clip (frame 63): its lanes
+// still run the FFT so that the prefetch loads issued inside fe_rest execute.
+constexpr int kDummyRowOff = kImgEnd;
+constexpr int kFusedLds = kDummyRowOff + kPRow + 1;
 static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 
 // kCtrlLFree + w (w = CNN wave 0..7): clips whose log-mel buffer CNN wave w
@@ -187,6 +190,16 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
     }
   };
 
+  // Part k of the prefetch (fe_rest calls it at four points of the round).
+  auto prefetch_part = [&](int64_t i, int r, Raw<T>& dst, int k) {
+    if (i < n_mine) {
+      const int fl = wave + 8 * r + slot_base;
+      const bool general = (r == 0 && wave == 0) || (r == 1 && wave == 6);   // frame 0 / frame 62
+      load_raw_part<true>(make_rsrc(audio + clip_of(i) * clip_stride, kWinSamples * sizeof(T)), 256 * fl - 160, j,
+                          kWinSamples, fl < kNFramesB, general, dst, k);
+    }
+  };
+
   Raw<T> pf;
   prefetch(0, 0, pf);
   WK_STAMP_INIT
@@ -205,22 +218,29 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: time the wait for the prefetched audio apart
       WK_STAMP(11);
 #endif
-      if (fl < kNFramesB) fe_stage0<true>(pf, 256 * fl - 160, kWinSamples, j, general, tb, a);
+      // Every lane runs the round (the frame-63 slot into a scratch row) so
+      // the prefetch parts issued from inside fe_rest load for all lanes.
+      fe_stage0<true>(pf, 256 * fl - 160, kWinSamples, j, general, tb, a);
       WK_STAMP(0);
-      prefetch(r == 0 ? i : i + 1, r ^ 1, pf);
+      const int64_t ni = r == 0 ? i : i + 1;
+      const int nr = r ^ 1;
+      auto pf_part = [&](int k) { prefetch_part(ni, nr, pf, k); };
       WK_STAMP(1);
       if (r == 0) {
         spin_until(ctrl, kCtrlFeBar, p_wait);   // every wave done reading clip i-1's power rows
         WK_STAMP(9);
       }
-      if (fl < kNFramesB) fe_rest<true>(a, j, lane, P + fl * kPRow, tb, w512, 0 WK_SP_ARG);
+      float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
+      fe_rest<true>(a, j, lane, row, tb, w512, 0, pf_part WK_SP_ARG);
     }
     if (exp_flags & 4) __builtin_amdgcn_s_setprio(1); else if (exp_flags & 8) __builtin_amdgcn_s_setprio(0);
     role_sync(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
     WK_STAMP(7);
     if (i >= 2 && !(exp_flags & 1)) spin_until_all8(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
     WK_STAMP(10);
+#ifndef WK_ABL_NOMEL
     mel_dispatch<true>(wave, P + min(lane, kNFramesB - 1) * kPRow, (i & 1 ? L1 : L) + lane);
+#endif
     WK_STAMP(8);
     signal_add(ctrl, kCtrlLReady, lane);
     // Split barrier: arrive now, wait before this wave next writes a power
