@@ -194,6 +194,83 @@ __device__ __forceinline__ void conv_pair_v(const float* __restrict__ img, const
   }
 }
 
+// ---- fp32 convolutions by Winograd F(2,3) (the fp32 path) ---------------
+// conv1d k3 p1 (cross-correlation) for the output pair (2p, 2p+1) from the
+// four input rows d_r = x[2p - 1 + r] (image rows 2p + r):
+//   m0 = (d0 - d2) g0,  m1 = (d1 + d2) (g0 + g1 + g2) / 2,
+//   m2 = (d2 - d1) (g0 - g1 + g2) / 2,  m3 = (d1 - d3) g2,
+//   y(2p) = m0 + m1 + m2,  y(2p+1) = m1 - m2 - m3.
+// Four products per input channel for two outputs instead of six: 2/3 of the
+// direct form's v_mfma_f32_16x16x4f32 work (on gfx950 the fp32 MFMA shares
+// the fp32 datapath with the front-end's VALU, so every MFMA cycle saved is a
+// front-end cycle).  The pair is also exactly maxpool(2)'s window, so the
+// epilogue pools in-lane.  MFMA columns = pairs; lane (n, q) reads rows
+// 2n..2n+3 at ci = 16 cb + 4 q + j (the ci-blocked K order of conv_pair_v, so
+// the same packed taps g0, g1, g2 serve; G1, G2 are formed per step).
+// boff = this lane's element of row 2n; image pitch CIP = 4 mod 8 keeps the
+// stride-2 row reads conflict-free.
+template <int CB, int CIP, int CHUNK = 0>
+__device__ __forceinline__ void conv_wino_v(const float* __restrict__ img, const float (&w)[12 * CB], int boff,
+                                            f32x4 (&m)[4]) {
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    float d[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float4 v = *reinterpret_cast<const float4*>(img + boff + r * CIP + 16 * cb);
+      d[r][0] = v.x;
+      d[r][1] = v.y;
+      d[r][2] = v.z;
+      d[r][3] = v.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float g0 = w[4 * cb + j], g1 = w[4 * (CB + cb) + j], g2 = w[4 * (2 * CB + cb) + j];
+      float sg = g0 + g2;
+      asm volatile("" : "+v"(sg));   // keep G1, G2 per step: hoisted out of the caller's loops they cost 2 VGPRs each
+      const float G1 = 0.5f * (sg + g1), G2 = 0.5f * (sg - g1);
+      m[0] = mfma4(g0, d[0][j] - d[2][j], m[0]);
+      m[1] = mfma4(G1, d[1][j] + d[2][j], m[1]);
+      m[2] = mfma4(G2, d[2][j] - d[1][j], m[2]);
+      m[3] = mfma4(g2, d[1][j] - d[3][j], m[3]);
+    }
+    if (CHUNK > 0 && (cb % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Winograd output transform + ReLU + maxpool(2): pair p -> pooled row p.
+template <int CIP_N, int TP_N, int TN>
+__device__ __forceinline__ void epi_wino_pool(const f32x4 (&m)[4], float* __restrict__ next, int co0, int clip, int p0,
+                                              int lane) {
+  const int p = p0 + (lane & 15);
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float y0 = m[0][r] + m[1][r] + m[2][r], y1 = m[1][r] - m[2][r] - m[3][r];
+    v[r] = fmaxf(fmaxf(y0, y1), 0.0f);
+  }
+  if (p < TN)
+    *reinterpret_cast<float4*>(next + (clip * TP_N + 1 + p) * CIP_N + co0 + 4 * (lane >> 4)) =
+        make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// conv3's tile holds two clips (columns 0-7: clip ca, 8-15: clip ca + 1; 8
+// pairs each, the 8th dropped by the floor pool): pooled -> mean over the 7.
+template <int GSTRIDE>
+__device__ __forceinline__ void epi_wino_gap(const f32x4 (&m)[4], float* __restrict__ g, int co0, int ca, int lane) {
+  const int p = lane & 7;
+  const int clip = ca + ((lane >> 3) & 1);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float y0 = m[0][r] + m[1][r] + m[2][r], y1 = m[1][r] - m[2][r] - m[3][r];
+    float s = p < 7 ? fmaxf(fmaxf(y0, y1), 0.0f) : 0.0f;
+    s += dpp<0xB1>(s);    // 8-lane sum: quad_perm xor 1, xor 2, row_half_mirror
+    s += dpp<0x4E>(s);
+    s += dpp<0x141>(s);
+    if (p == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s / 7.0f;
+  }
+}
+
 // ReLU -> maxpool(2) -> this lane's 4 pooled channels (consecutive co) as one
 // 16-byte store into the next layer's fp32 [clip][t][ci] image.
 template <int CIP_N, int TP_N, int TN>

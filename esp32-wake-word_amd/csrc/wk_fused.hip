@@ -58,11 +58,17 @@ constexpr int I0_CIP = 24, I1_CIP = 40, I2_CIP = 72;                 // elements
 // next clip's (or the next image's) rows, which only affects their own MFMA
 // columns.  conv3 keeps 2 spare rows so its last clip stays inside the carve.
 constexpr int I0_TP = 64, I1_TP = 32, I2_TP = 18;
-// fp32 images (float units)
+// fp32 images (float units), read by the Winograd convolutions in row pairs:
+// pitch = 4 mod 8 floats keeps the stride-2 row reads conflict-free.
+constexpr int F0_CIP = 20, F1_CIP = 36, F2_CIP = 68;
 constexpr int kF0Off = kImgOff;
-constexpr int kF1Off = kF0Off + NBF * I0_TP * I0_CIP;
-constexpr int kF2Off = kF1Off + NBF * I1_TP * I1_CIP;
-constexpr int kImgEnd = kF2Off + NBF * I2_TP * I2_CIP;
+constexpr int kF1Off = kF0Off + NBF * I0_TP * F0_CIP;
+constexpr int kF2Off = kF1Off + NBF * I1_TP * F1_CIP;
+constexpr int kF2End = kF2Off + NBF * I2_TP * F2_CIP;
+// bf16 images (the largest user of the carve is the split-bf16 set below)
+constexpr int kImgEnd = kImgOff + NBF * (I0_TP * 40 + I1_TP * 72 + I2_TP * 136) / 2 > kF2End
+                            ? kImgOff + NBF * (I0_TP * 40 + I1_TP * 72 + I2_TP * 136) / 2
+                            : kF2End;
 // bf16 images (offsets in float units)
 constexpr int kB0Off = kImgOff;
 constexpr int kB1Off = kB0Off + NBF * I0_TP * I0_CIP / 2;
@@ -294,7 +300,10 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 #pragma unroll
     for (int s = 0; s < 12; ++s) w3b[s] = frag_bf(kPbW3 + (cw * 12 + s) * 256);
   }
-  if constexpr (CM == kConvF32) {
+#ifndef WK_W3_RESIDENT
+#define WK_W3_RESIDENT 1   // fp32 conv3 taps in VGPRs across batches (1; measured +5 %) or re-read from L2 per pass (0)
+#endif
+  if constexpr (CM == kConvF32 && WK_W3_RESIDENT) {
 #pragma unroll
     for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
   }
@@ -329,7 +338,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         if (!(exp_flags & 2)) spin_until(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
         const float* lrow = (i & 1 ? L1 : L) + ln;
         const int k = (cw + 3 * s) & 7;
-        float* f0 = F0 + (s * I0_TP + 1 + ln) * I0_CIP;
+        float* f0 = F0 + (s * I0_TP + 1 + ln) * F0_CIP;
         uint16_t* f0b = B0 + (s * I0_TP + 1 + ln) * I0_CIP;
         uint16_t* f0x = X0 + (s * I0_TP + 1 + ln) * X0_CIP;
         float* fo = feats_out ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) + ln : nullptr;
@@ -393,9 +402,10 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
           epi_pool_bf3<X1_CIP, I1_TP, 31, 32>(acc_a, X1, co0, cl, ta, lane);
           epi_pool_bf3<X1_CIP, I1_TP, 31, 32>(acc_b, X1, co0, cl, tb, lane);
         } else {
-          conv_pair_v<1, I0_CIP, 1>(F0, w1, bo + ta * I0_CIP, bo + tb * I0_CIP, acc_a, acc_b);
-          epi_pool_v<I1_CIP, I1_TP, 31>(acc_a, F1, co0, cl, ta, lane);
-          epi_pool_v<I1_CIP, I1_TP, 31>(acc_b, F1, co0, cl, tb, lane);
+          // Winograd pairs 16 p .. 16 p + 15 (outputs 32 p .. 32 p + 31)
+          f32x4 m[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+          conv_wino_v<1, F0_CIP>(F0, w1, (cl * I0_TP + 2 * (16 * p + li)) * F0_CIP + 4 * lk, m);
+          epi_wino_pool<F1_CIP, I1_TP, 31>(m, F1, co0, cl, 16 * p, lane);
         }
       }
     }
@@ -442,11 +452,9 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
-        const int bo = (cl * I1_TP + li) * I1_CIP + 4 * lk;
-        f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
-        conv_pair_v<2, I1_CIP, 2>(F1, w2, bo, bo + 16 * I1_CIP, acc_a, acc_b);
-        epi_pool_v<I2_CIP, I2_TP, 15>(acc_a, F2, co0, cl, 0, lane);
-        epi_pool_v<I2_CIP, I2_TP, 15>(acc_b, F2, co0, cl, 16, lane);
+        f32x4 m[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+        conv_wino_v<2, F1_CIP, 1>(F1, w2, (cl * I1_TP + 2 * li) * F1_CIP + 4 * lk, m);
+        epi_wino_pool<F2_CIP, I2_TP, 15>(m, F2, co0, cl, 0, lane);
       }
     }
     WK_STAMP(3);
@@ -471,7 +479,15 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
           conv_pair_bf3<12, 4, X2_CIP, 3>(X2, w3b, w3l, bx + ca * I2_TP * X2_CIP, bx + cb * I2_TP * X2_CIP, acc_a,
                                           acc_b);
         } else {
-          conv_pair_v<4, I2_CIP, 2>(F2, w3, bo + ca * I2_TP * I2_CIP, bo + cb * I2_TP * I2_CIP, acc_a, acc_b);
+          // Winograd: one tile of 16 pair columns = 8 pairs of clip ca, 8 of clip cb
+          if (!WK_W3_RESIDENT) {
+#pragma unroll
+            for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
+          }
+          f32x4 m[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+          conv_wino_v<4, F2_CIP, 1>(F2, w3, ((ca + (li >> 3)) * I2_TP + 2 * (li & 7)) * F2_CIP + 4 * lk, m);
+          epi_wino_gap<NBF>(m, Gp, co0, ca, lane);
+          continue;
         }
         epi_gap<NBF>(acc_a, Gp, co0, ca, lane);
         epi_gap<NBF>(acc_b, Gp, co0, cb, lane);
