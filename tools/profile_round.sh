@@ -35,7 +35,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 cd "$R"
 timeout -k 10 900 bash tools/profile_pmc.sh "$OUT/pmc" --steps 2 --warmup 1 --no-cpu-baseline $BARGS > "$OUT/pmc.log" 2>&1
 python3 tools/pmc_summary.py "$OUT/pmc" --json "$OUT/${TAG}_pmc.json" > "$OUT/pmc_summary.txt"
-case "$BARGS" in *bf16*) BF=true; TF=hbm_traffic_bf16.json ;; *) BF=false; TF=hbm_traffic.json ;; esac
+case "$BARGS" in *bf16x3*) BF=2; TF=hbm_traffic_bf16x3.json ;; *bf16*) BF=1; TF=hbm_traffic_bf16.json ;; *) BF=0; TF=hbm_traffic.json ;; esac
 python3 - "$OUT/${TAG}_pmc.json" "$OUT/$TF" "$TAG" "$BF" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
