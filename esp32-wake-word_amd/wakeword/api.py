@@ -263,3 +263,17 @@ def extract_mfcc(signal: Iterable[float], signal_len: Optional[int] = None, samp
     out = np.ctypeslib.as_array(p, shape=(nf * n_mfcc,)).copy().reshape(nf, n_mfcc)
     L.free_mfcc(p)
     return out
+
+
+_DEFAULT_MODELS: Dict[tuple, "KWSModel"] = {}
+
+
+def detect(wave_batch, onnx: Optional[str] = None, device: int = 0, precision: str = "fp32"):
+    """(B, 16000) float32/int16 audio -> logits (B,) on device, with a cached
+    model per (onnx, device, precision); onnx defaults to $WAKEWORD_ONNX or the
+    xiaoa.onnx kept with the test fixtures (wakeword.test.default_onnx)."""
+    from .test import default_onnx
+    key = (onnx or default_onnx(), device, precision)
+    if key not in _DEFAULT_MODELS:
+        _DEFAULT_MODELS[key] = load_onnx(key[0], device=device, precision=precision)
+    return _DEFAULT_MODELS[key].detect(wave_batch)

@@ -150,3 +150,23 @@ def test_frontend_raw_mfcc_every_frame(gpu):
     gi = wakeword.mfcc(xi, cmvn=False).cpu().numpy()
     ri = O.mfcc_torchaudio(xi.astype(np.float32) / 32768.0)
     assert np.abs(gi - ri).max() < 1e-3
+
+
+def test_cli_config1_golden_wavs(gpu, golden_dir, capsys):
+    """python -m wakeword.test (config 1): WAV -> zero pad -> logit, against the
+    reference LightweightKWS logits of the zero-padded golden WAVs."""
+    import json as _json
+    import wakeword
+    from wakeword import test as cli
+    g = np.load(os.path.join(golden_dir, "wavs.npz"))
+    paths = [os.path.join(golden_dir, "wav", str(n)) for n in g["name"]]
+    assert cli.main([*paths, "--pad", "zero", "--json"]) == 0
+    rows = [_json.loads(s) for s in capsys.readouterr().out.strip().splitlines()]
+    got = np.array([r["logit"] for r in rows])
+    assert np.abs(got - g["logit_zero"]).max() < LOGIT_ATOL
+    for r in rows:
+        assert abs(r["probability"] - 1.0 / (1.0 + np.exp(-r["logit"]))) < 1e-9
+        assert r["wake"] == (r["probability"] > 0.5)
+    # the module-level detect() is the same model
+    lz = wakeword.detect(cli.prepare(paths, "zero")).cpu().numpy()
+    assert np.abs(lz - got).max() < 1e-6

@@ -102,3 +102,20 @@ def test_augment_matches_torch_interpolate():
     v = wav.augment(x * 4, volume=1.3, out_len=x.size)
     np.testing.assert_array_equal(v, np.clip(x * 4 * np.float32(1.3), -1, 1))
     assert len(wav.augment_variants(x)) == 5
+
+
+def test_cli_prepare_zero_pad_matches_wave_module(golden_dir):
+    """The config-1 CLI's host side: native WAV read + zero pad (no GPU)."""
+    import wave as _wave
+    from wakeword import test as cli
+    p = os.path.join(golden_dir, "wav", "xiaoa_095.wav")
+    x = cli.prepare([p], "zero")
+    with _wave.open(p) as w:
+        raw = np.frombuffer(w.readframes(w.getnframes()), "<i2")[:16000].astype(np.float32) / 32768.0
+    assert x.shape == (1, 16000) and x.dtype == np.float32
+    np.testing.assert_array_equal(x[0, :raw.size], raw)
+    assert not x[0, raw.size:].any()
+    xn = cli.prepare([p], "noise", seed=3)
+    np.testing.assert_array_equal(xn[0, :raw.size], raw)
+    assert 0.002 < xn[0, raw.size:].std() < 0.008
+    assert cli.prepare([], "zero").shape == (0, 16000)
