@@ -8,6 +8,9 @@
 #ifndef WK_SPLIT_G
 #define WK_SPLIT_G 3   // real-FFT split chains interleaved per group (fe_rest)
 #endif
+#ifndef WK_SPLIT_MIRROR
+#define WK_SPLIT_MIRROR 0   // 1: second-pass columns placed so real-FFT split partners are row mirrors (one DPP)
+#endif
 #ifndef WK_TW_GROUP
 #define WK_TW_GROUP 0   // >0: fence the twiddle LDS reads into groups of this many (0 = compiler schedules; measured equal)
 #endif
@@ -116,6 +119,16 @@ __device__ __forceinline__ void load_raw_part(__amdgpu_buffer_rsrc_t rs, int bas
   if (part == 0) r.xb = raw_ld<T>(rs, base - 1);
 }
 
+// Column k1 of the second DFT16 pass held by lane j of a 16-lane group.
+// Plain: k1 = j; the split partner column 16 - k1 then sits in lane 16 - j
+// (two DPP moves).  Mirrored (WK_SPLIT_MIRROR): columns 1-7 in lanes 1-7,
+// 9-15 in lanes 8-14, 0 in lane 0, 8 in lane 15 -- the partner of the column
+// in lane j is in lane 15 - j (DPP row_mirror), and the two self-partnered
+// columns 0 and 8 sit in lanes 0 and 15.
+__device__ __forceinline__ constexpr int fe_kcol(int j) {
+  return WK_SPLIT_MIRROR ? (j < 8 ? j : (j == 15 ? 8 : j + 1)) : j;
+}
+
 struct NoPrefetch {
   __device__ __forceinline__ void operator()(int) const {}
 };
@@ -216,18 +229,20 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
   pf(1);
   f2 c[16];
 #ifdef WK_ABL_NOTRANS
+  const int kc = fe_kcol(j);
 #pragma unroll
   for (int n2 = 0; n2 < 16; ++n2) c[n2] = b[n2];
 #else
+  const int kc = fe_kcol(j);   // the column this lane transforms in the second pass
   wave_lds_sync();
 #pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) c[n2].x = row[17 * j + n2];
+  for (int n2 = 0; n2 < 16; ++n2) c[n2].x = row[17 * kc + n2];
   wave_lds_sync();
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) row[17 * k1 + j] = b[k1].y;
   wave_lds_sync();
 #pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) c[n2].y = row[17 * j + n2];
+  for (int n2 = 0; n2 < 16; ++n2) c[n2].y = row[17 * kc + n2];
   wave_lds_sync();
 #endif
   WK_FE_HIT(4);
@@ -280,6 +295,13 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
       if (k2 < 8) {
         const f2 sv = c[dft16_out(15 - k2)];
         const f2 own = c[dft16_out((16 - k2) & 15)];
+#if WK_SPLIT_MIRROR
+        // lane 15 - j holds the partner column; lanes 0 (column 0) and 15
+        // (column 8) are their own partners: registers (16 - k2) & 15 / 15 - k2.
+        const float pr = dpp<0x140>(sv.x);
+        const float pi = dpp<0x140>(sv.y);
+        zq = j == 0 ? own : (j == 15 ? sv : f2{pr, pi});
+#else
 #ifdef WK_SPLIT_BPERMUTE
         const float pr = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sv.x)));
         const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sv.y)));
@@ -288,6 +310,7 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
         const float pi = dpp<0x121>(dpp<0x140>(sv.y));
 #endif
         zq = j == 0 ? own : f2{pr, pi};
+#endif
       } else {
         zq = c[dft16_out(8)];
       }
@@ -315,7 +338,7 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
     for (int t = 0; t < G; ++t) {
       const int k2 = k0 + t;
       if (k2 > 8) continue;
-      const int kb = j + 16 * k2;
+      const int kb = kc + 16 * k2;
       if (k2 < 8) {
         row[kb] = pw[t].x;
         row[256 - kb] = pw[t].y;
@@ -396,5 +419,6 @@ __device__ __forceinline__ f2 fe_w512(int j) {
   sincospif(-(float)j / 256.0f, &sn, &cs);
   return f2{cs, sn};
 }
+__device__ __forceinline__ f2 fe_w512_lane(int j) { return fe_w512(fe_kcol(j)); }   // W512^k1 of the lane's column
 
 }  // namespace wk

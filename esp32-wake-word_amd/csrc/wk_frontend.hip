@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
 
   fe_init_tables<MODE_B>(smem, threadIdx.x, kFeBlock);
   const FeTables tb = {smem + kWinOff, smem + kTwOff};
-  const f2 w512 = fe_w512(j);
+  const f2 w512 = fe_w512_lane(j);
   // Frame slots: groups 0/1 (and 2/3) of a wave take frames 16 apart so their
   // pitch-17 transpose images fall in disjoint LDS banks.
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);

@@ -7,7 +7,8 @@
 // the lane-per-frame mel filterbank of wk_fe_dev.h clip after clip and write
 // each clip's log-mel image [40][63] into one of two LDS buffers.  Waves 8-15
 // (CNN role) take the DCT-II + CMVN from that buffer into the conv1 input
-// image, then run the CNN of wk_cnn.hip on batches of NBF = 4 clips.  The
+// image (one wave per clip, on the matrix cores: dct_cmvn_clip), then run the
+// CNN of wk_cnn.hip on batches of NBF = 4 clips.  The
 // roles share no s_barrier: each synchronises its own 8 waves through an LDS
 // counter barrier, and the hand-off is two LDS counters (log-mel ready /
 // log-mel buffer free).  Moving the DCT + CMVN to the CNN waves (which wait
@@ -40,15 +41,19 @@ __device__ unsigned long long g_wk_stamps[16][16];
 #endif
 
 constexpr int NBF = 4;               // clips per CNN batch
+#ifndef WK_DCT_EAGER
+#define WK_DCT_EAGER 1               // MFMA DCT of the next batch's clips between this batch's conv phases
+#endif
 constexpr int kFusedBlock = 1024;    // 8 front-end + 8 CNN waves
 // LDS carve after the front-end's (wk_fe_dev.h): fixed tail, then the CNN
 // images [clip][t][ci] -- fp32, or bf16 for bf16 convolutions -- overlaying
 // one region.  ci pitch = 8 mod 16 elements: the 16 t-lanes of each lane
 // group of a B-fragment read (ds_read_b128 fp32 / ds_read_b64 bf16) and of the
 // pooled stores land on distinct banks.
-constexpr int kGOff = kFeLds;                       // pooled features [128][4]
+constexpr int kGOff = (kFeLds + 3) & ~3;            // pooled features [128][4] (16-byte aligned carve below)
 constexpr int kFcpOff = kGOff + 128 * NBF;          // classifier.0 partials [2][64][4]
 constexpr int kL1Off = kFcpOff + 2 * 64 * NBF;      // second log-mel buffer [40][64] (first: kLOff)
+static_assert(kLOff % 4 == 0 && kL1Off % 4 == 0, "log-mel buffers are read with ds_read_b128");
 constexpr int kCtrlOff = kL1Off + kLSize;           // control words
 constexpr int kImgOff = (kCtrlOff + 16 + 3) & ~3;   // 16-byte aligned
 constexpr int I0_CIP = 24, I1_CIP = 40, I2_CIP = 72;                 // elements (= 8 mod 16)
@@ -177,8 +182,14 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   unsigned* ctrl = reinterpret_cast<unsigned*>(smem + kCtrlOff);
   const int g = lane >> 4, j = lane & 15;
   const FeTables tb = {smem + kWinOff, smem + kTwOff};
-  const f2 w512 = fe_w512(j);
+  const f2 w512 = fe_w512_lane(j);
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);
+  const int fw = wave;   // frame slot of this wave (moving the edge frames to other waves measured neutral)
+#ifdef WK_ABL_NOEDGE
+  constexpr bool kEdge = false;   // timing ablation (tools/debug): edge frames take the plain path (wrong results)
+#else
+  constexpr bool kEdge = true;
+#endif
   const int64_t G = gridDim.x;
   unsigned gen = 0, p_wait = 0;
 
@@ -189,8 +200,8 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   auto clip_of = [&](int64_t i) { return (int64_t)blockIdx.x + G * i; };
   auto prefetch = [&](int64_t i, int r, Raw<T>& dst) {
     if (i < n_mine) {
-      const int fl = wave + 8 * r + slot_base;
-      const bool general = (r == 0 && wave == 0) || (r == 1 && wave == 6);   // frame 0 / frame 62
+      const int fl = fw + 8 * r + slot_base;
+      const bool general = kEdge && ((r == 0 && fw == 0) || (r == 1 && fw == 6));   // frame 0 / frame 62
       load_raw<true>(make_rsrc(audio + clip_of(i) * clip_stride, kWinSamples * sizeof(T)), 256 * fl - 160, j,
                      kWinSamples, fl < kNFramesB, general, dst);
     }
@@ -199,8 +210,8 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   // Part k of the prefetch (fe_rest calls it at four points of the round).
   auto prefetch_part = [&](int64_t i, int r, Raw<T>& dst, int k) {
     if (i < n_mine) {
-      const int fl = wave + 8 * r + slot_base;
-      const bool general = (r == 0 && wave == 0) || (r == 1 && wave == 6);   // frame 0 / frame 62
+      const int fl = fw + 8 * r + slot_base;
+      const bool general = kEdge && ((r == 0 && fw == 0) || (r == 1 && fw == 6));   // frame 0 / frame 62
       load_raw_part<true>(make_rsrc(audio + clip_of(i) * clip_stride, kWinSamples * sizeof(T)), 256 * fl - 160, j,
                           kWinSamples, fl < kNFramesB, general, dst, k);
     }
@@ -212,8 +223,8 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   for (int64_t i = 0; i < n_mine; ++i) {
 #pragma unroll 1
     for (int r = 0; r < 2; ++r) {
-      const int fl = wave + 8 * r + slot_base;   // == frame index t (one chunk per clip)
-      const bool general = (r == 0 && wave == 0) || (r == 1 && wave == 6);
+      const int fl = fw + 8 * r + slot_base;   // == frame index t (one chunk per clip)
+      const bool general = kEdge && ((r == 0 && fw == 0) || (r == 1 && fw == 6));
       if (exp_flags & 4) {   // alternate issue priority between the two front-end waves of a SIMD
         if ((wave >= 4) == (r == 1)) __builtin_amdgcn_s_setprio(2); else __builtin_amdgcn_s_setprio(1);
       } else if (exp_flags & 8) {
@@ -256,6 +267,97 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
     p_wait = gen;
   }
   WK_STAMP_FLUSH(wave);
+}
+
+// ---------------------------------------------------------------------------
+// DCT-II + CMVN of one clip on the matrix cores (extract_mfcc.py:70-80; the
+// DCT of torchaudio.transforms.MFCC, ortho, 13 of 40): the 13x40 DCT (rows
+// 13-15 zero) times the [40 mel][64 frame] log-mel image is a 16x40x64 fp32
+// GEMM = 10 K-steps x 4 column tiles of v_mfma_f32_16x16x4f32, run by ONE wave.
+// Column li of tile nt is frame 4 li + nt, so a lane's B values of one K-step
+// are 4 consecutive frames: one ds_read_b128 feeds the 4 tiles.  The lane then
+// holds coefficients 4 lk .. 4 lk + 3 of frames 4 li .. 4 li + 3: CMVN's
+// per-coefficient sums are 3 in-register adds + a 16-lane DPP row reduction,
+// and the 4 normalised coefficients of a frame leave as one 16-byte (fp32) or
+// 8-byte (bf16) store into the conv1 image [clip][t][ci].  Frame 63 (column
+// 15 of tile 3) is a padding column: excluded from the statistics, not stored.
+// (Replaces 13 x 40 lane-per-frame FMAs + 13 separate wave reductions spread
+// over the 8 CNN waves: ~1,300 VALU instructions per clip -> 40 MFMA + ~150.)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float row_sum16(float v) {   // sum over the lane's 16-lane row, in every lane
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  v += dpp<0x140>(v);  // row_mirror
+  return v;
+}
+
+template <int CM>
+__device__ __forceinline__ void dct_cmvn_clip(const float* __restrict__ lbuf, int slot, float* __restrict__ F0,
+                                              uint16_t* __restrict__ B0, uint16_t* __restrict__ X0,
+                                              float* __restrict__ fo, int lane) {
+  const int li = lane & 15, lk = lane >> 4;
+  // A fragments kDctB16[li][4 s + lk], re-read (L1/L2-resident, 2.5 KB) per
+  // clip: kept live across the batch they pushed the fp32 CNN into spills.
+  int aoff = 4 * (li * 40 + lk);
+  asm volatile("" : "+v"(aoff));   // not loop-invariant: keep the loads here
+  const auto ra = make_rsrc(kDctB16, sizeof(kDctB16));
+  float dA[10];
+#pragma unroll
+  for (int s = 0; s < 10; ++s) dA[s] = buf_load(ra, aoff, 16 * s);
+  f32x4 d[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+  for (int s = 0; s < 10; ++s) {
+    const f32x4 b = *reinterpret_cast<const f32x4*>(lbuf + (4 * s + lk) * WK_LSTRIDE + 4 * li);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) d[nt] = mfma4(dA[s], b[nt], d[nt]);
+  }
+  const bool v3 = li != 15;   // tile 3 column 15 = frame 63 (padding)
+  float mean[4], inv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float x3 = v3 ? d[3][r] : 0.0f;
+    mean[r] = row_sum16((d[0][r] + d[1][r]) + (d[2][r] + x3)) / (float)kNFramesB;
+    float dv[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dv[nt] = d[nt][r] - mean[r];
+    dv[3] = v3 ? dv[3] : 0.0f;
+    const float q = row_sum16((dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]));
+    float sd = sqrtf(q / (float)(kNFramesB - 1));
+    sd = sd == 0.0f ? 1.0f : sd;   // rows 13-15 (all zero) land here and stay 0
+    inv[r] = 1.0f / (sd + 1e-8f);
+  }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int t = 4 * li + nt;
+    if (nt == 3 && !v3) continue;
+    const int row = slot * I0_TP + 1 + t;
+    float y[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = (d[nt][r] - mean[r]) * inv[r];
+    if constexpr (CM == kConvBf16) {
+      uint2 pk;
+      pk.x = bf16_bits(y[0]) | (bf16_bits(y[1]) << 16);
+      pk.y = bf16_bits(y[2]) | (bf16_bits(y[3]) << 16);
+      *reinterpret_cast<uint2*>(B0 + row * I0_CIP + 4 * lk) = pk;
+    } else if constexpr (CM == kConvBf16x3) {
+      uint32_t h[4], l[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        h[r] = bf16_bits(y[r]);
+        l[r] = bf16_bits(y[r] - __uint_as_float(h[r] << 16));
+      }
+      *reinterpret_cast<uint2*>(X0 + row * X0_CIP + 4 * lk) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+      *reinterpret_cast<uint2*>(X0 + row * X0_CIP + 16 + 4 * lk) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+    } else {
+      *reinterpret_cast<f32x4*>(F0 + row * F0_CIP + 4 * lk) = f32x4{y[0], y[1], y[2], y[3]};
+    }
+    if (fo) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * lk + r < 13) fo[(4 * lk + r) * kNFramesB + t] = y[r];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -308,8 +410,45 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
   }
   const int64_t n_batches = (n_mine + NBF - 1) / NBF;
+  // Log-mel buffer release (kCtrlLFree + w): wave w < NBF reads only clips
+  // w, w + NBF, w + 2 NBF, ...; its word holds the next clip it will read, so
+  // every clip below it is released.  Waves >= NBF read none.
+  signal_set(ctrl, kCtrlLFree + cw, cw < NBF ? (unsigned)cw : 0xFFFFFFFFu, lane);
+  bool eager_done = false;
+  auto dct_clip = [&](int64_t i, int slot) {
+    float* fo = feats_out ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) : nullptr;
+    dct_cmvn_clip<CM>(i & 1 ? L1 : L, slot, F0, B0, X0, fo, lane);
+    signal_set(ctrl, kCtrlLFree + cw, (unsigned)(i + NBF), lane);
+  };
+  // Between the conv phases of batch b (after its conv1 has consumed the conv1
+  // image): if the log-mel of clip 4(b+1) + cw is already there, take its DCT
+  // now, so its buffer goes back to the front-end a whole batch earlier (the
+  // double buffer otherwise stalled the front-end ~13 % of the time in fp32).
+  auto try_eager = [&](int64_t b) {
+    if (!WK_DCT_EAGER || cw >= NBF || eager_done) return;
+    const int64_t i = (b + 1) * NBF + cw;
+    if (i >= n_mine) return;
+    const bool ready = (exp_flags & 2) ||
+                       __builtin_amdgcn_readfirstlane(lds_load(ctrl + kCtrlLReady)) >= 8u * (unsigned)(i + 1);
+    if (ready) {
+      dct_clip(i, cw);
+      eager_done = true;
+    }
+  };
   WK_STAMP_INIT
   for (int64_t b = 0; b < n_batches; ++b) {
+    // DCT-II + CMVN (extract_mfcc.py:70-80): CNN wave s < NBF takes clip
+    // 4b + s whole on the matrix cores (dct_cmvn_clip), unless it already did
+    // so eagerly during the previous batch (try_eager below).
+    if (cw < NBF && !eager_done) {
+      const int64_t i = b * NBF + cw;
+      if (i < n_mine) {
+        if (!(exp_flags & 2)) spin_until(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
+        dct_clip(i, cw);
+      }
+    }
+    eager_done = false;
+    // conv1's A fragments: loaded after the DCT (register pressure), landing during the sync.
     float w1[12];
     s4 w1b[3], w1l[3];
     if constexpr (BF || X3) {
@@ -323,63 +462,6 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     if constexpr (CM == kConvF32) {
 #pragma unroll
       for (int s = 0; s < 12; ++s) w1[s] = buf_load(rs, lv, 4 * (kPkW1 + ((cw & 1) * 12 + s) * 64));
-    }
-    // DCT-II + CMVN of the batch's clips (extract_mfcc.py:70-80) from the
-    // double-buffered log-mel image into the conv1 input image.  Coefficient
-    // sets (k < 5: coefficients 2k, 2k+1; k >= 5: k+5) rotate over the waves
-    // per clip, so over a batch every wave does 6 or 7 coefficients.
-    {
-      const int nb = (int)(n_mine - b * NBF < NBF ? n_mine - b * NBF : NBF);
-      int ln = lane;
-      asm volatile("" : "+v"(ln));   // keep lane addressing out of the loop-invariant (spilled) set
-      const bool valid = ln < kNFramesB;
-      for (int s = 0; s < nb; ++s) {
-        const int64_t i = b * NBF + s;
-        if (!(exp_flags & 2)) spin_until(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
-        const float* lrow = (i & 1 ? L1 : L) + ln;
-        const int k = (cw + 3 * s) & 7;
-        float* f0 = F0 + (s * I0_TP + 1 + ln) * F0_CIP;
-        uint16_t* f0b = B0 + (s * I0_TP + 1 + ln) * I0_CIP;
-        uint16_t* f0x = X0 + (s * I0_TP + 1 + ln) * X0_CIP;
-        float* fo = feats_out ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) + ln : nullptr;
-        if (k < 5) {
-          const int c0 = 2 * k;
-          float y0 = dct_coef<true>(c0, lrow), y1 = dct_coef<true>(c0 + 1, lrow);
-          cmvn_lane2(y0, y1, valid, kNFramesB);
-          if (valid && BF) {
-            *reinterpret_cast<uint32_t*>(f0b + c0) = bf16_bits(y0) | (bf16_bits(y1) << 16);   // c0 even
-          } else if (valid && X3) {
-            const uint32_t h0 = bf16_bits(y0), h1 = bf16_bits(y1);
-            *reinterpret_cast<uint32_t*>(f0x + c0) = h0 | (h1 << 16);
-            *reinterpret_cast<uint32_t*>(f0x + 16 + c0) =
-                bf16_bits(y0 - __uint_as_float(h0 << 16)) | (bf16_bits(y1 - __uint_as_float(h1 << 16)) << 16);
-          } else if (valid) {
-            *reinterpret_cast<float2*>(f0 + c0) = make_float2(y0, y1);   // c0 even
-          }
-          if (valid) {
-            if (fo) {
-              fo[c0 * kNFramesB] = y0;
-              fo[(c0 + 1) * kNFramesB] = y1;
-            }
-          }
-        } else {
-          const int c0 = k + 5;
-          const float y = cmvn_lane(dct_coef<true>(c0, lrow), valid, kNFramesB);
-          if (valid) {
-            if (BF) {
-              f0b[c0] = (uint16_t)bf16_bits(y);
-            } else if (X3) {
-              const uint32_t h = bf16_bits(y);
-              f0x[c0] = (uint16_t)h;
-              f0x[16 + c0] = (uint16_t)bf16_bits(y - __uint_as_float(h << 16));
-            } else {
-              f0[c0] = y;
-            }
-            if (fo) fo[c0 * kNFramesB] = y;
-          }
-        }
-        signal_set(ctrl, kCtrlLFree + cw, (unsigned)(i + 1), lane);   // this wave's reads of the log-mel buffer are done
-      }
     }
     WK_STAMP(0);
     role_sync(ctrl, kCtrlCnnBar, gen, lane);   // conv1 image complete
@@ -411,6 +493,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     }
     WK_STAMP(1);
     role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    try_eager(b);
     WK_STAMP(2);
 
     // conv2: co tile (cw&3), clips 2*(cw>>2) + {0,1}, 2 t-tiles each.
@@ -459,6 +542,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     }
     WK_STAMP(3);
     role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    try_eager(b);
     WK_STAMP(4);
 
     // conv3: co tile cw, the 4 clips; GAP -> G[128][4].
@@ -500,6 +584,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     }
     WK_STAMP(5);
     role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    try_eager(b);
     WK_STAMP(6);
 
     // classifier.0 (128 -> 64): o tile (cw&3), k half (cw>>2); columns >= NBF are don't-care.
@@ -541,6 +626,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
       const int64_t i = b * NBF + cl;
       if (q == 0 && i < n_mine) logits[(int64_t)blockIdx.x + G * i] = acc;
     }
+    try_eager(b);
     WK_STAMP(8);
 #ifdef WK_SYNC_AFTER_FC2
     role_sync(ctrl, kCtrlCnnBar, gen, lane);

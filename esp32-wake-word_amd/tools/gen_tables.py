@@ -203,6 +203,10 @@ def main():
         scale = math.sqrt(1.0 / N_MELS) if c == 0 else math.sqrt(2.0 / N_MELS)
         body = " ".join(f"s = __builtin_fmaf(l[{m} * WK_LSTRIDE], {f32(dA[c, m])}, s);" for m in range(N_MELS))
         out.append(f"__device__ __forceinline__ float dctA_{c}(const float* __restrict__ l) {{ float s = 0.0f; {body} return {f32(scale)} * s; }}")
+    # Mode B DCT as the A operand of a 16x40 fp32 MFMA GEMM (rows 13-15 zero).
+    dB16 = np.zeros((16, N_MELS), np.float32)
+    dB16[:N_MFCC] = dB
+    out.append("__constant__ float kDctB16[16 * 40] = {" + ", ".join(f32(v) for v in dB16.reshape(-1)) + "};")
     out.append("template <bool MODE_B> __device__ __forceinline__ float dct_coef(int c, const float* __restrict__ l) {")
     out.append("  switch (c) {")
     for c in range(N_MFCC):
