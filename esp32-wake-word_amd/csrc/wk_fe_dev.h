@@ -144,7 +144,11 @@ __device__ __forceinline__ float row_rol1(float v) {  // lane l <- lane (l+1) mo
 struct FeTables {
   const float* win;   // [320] analysis window (mode-specific)
   const float* tw;    // [15][16][2]: W256^(j*k1), k1 = 1..15
+  const float* tws;   // [7][16][2]: W512^(fe_kcol(j) + 16*k2), k2 = 1..7 (TWS kernels only), else null
 };
+
+// Fill the combined split twiddles of FeTables::tws (all threads of the WG).
+__device__ __forceinline__ void fe_init_tws(float* tws, int tid, int nthreads);
 
 // Stage 0: pre-emphasis + window of the 320 frame samples as 160 complex
 // (even, odd) pairs: lane j holds pair index 16*n1 + j, n1 = 0..9.
@@ -199,7 +203,10 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
 // Stages 1..4 of one frame -> its power row (bins 0..256) in LDS.  All
 // complex arithmetic is packed fp32 (see f2 in wk_common.h).
 // pf(k), k = 0..3, is called at four points of the round (prefetch parts).
-template <bool MODE_B, typename PF = NoPrefetch>
+// TWS: the split's twiddle W512^k, k = kc + 16 k2, is one table value per
+// (lane, k2) (tb.tws) instead of W512^kc x the constant W32^k2 -- one complex
+// multiply instead of two; bin 128 comes from |Z[128]|^2 directly.
+template <bool MODE_B, typename PF = NoPrefetch, bool TWS = false>
 __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __restrict__ row, const FeTables& tb,
                                         f2 w512, int esp_pack, const PF& pf = PF() WK_SP_PARAM) {
   pf(0);
@@ -283,13 +290,21 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
   return;
 #endif
   constexpr int G = WK_SPLIT_G;
+  constexpr int K2MAX = TWS ? 7 : 8;
+  if constexpr (TWS) {
+    // bin 128 (k2 = 8, column 0): X[128] = conj Z[128], so |U|^2 = 4 |Z[128]|^2.
+    const f2 z = c[dft16_out(8)];
+    float p128 = 4.0f * __builtin_fmaf(z.x, z.x, z.y * z.y);
+    if constexpr (!MODE_B) p128 = __builtin_fmaf(p128, sc.x, 1e-12f);
+    if (j == 0) row[128] = p128;
+  }
 #pragma unroll
-  for (int k0 = 0; k0 <= 8; k0 += G) {
+  for (int k0 = 0; k0 <= K2MAX; k0 += G) {
     f2 S[G], D[G], pw[G];
 #pragma unroll
     for (int t = 0; t < G; ++t) {
       const int k2 = k0 + t;
-      if (k2 > 8) continue;
+      if (k2 > K2MAX) continue;
       const f2 zk = c[dft16_out(k2)];
       f2 zq;
       if (k2 < 8) {
@@ -320,15 +335,17 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
 #pragma unroll
     for (int t = 0; t < G; ++t) {
       const int k2 = k0 + t;
-      if (k2 > 8) continue;
+      if (TWS || k2 > 8) continue;
       if (k2 == 8) D[t] = swp(D[t]) * f2{1.0f, -1.0f};   // W32^8 = -i
       else if (k2 > 0) D[t] = cmulc(D[t], w32(k2));
     }
 #pragma unroll
     for (int t = 0; t < G; ++t) {
       const int k2 = k0 + t;
-      if (k2 > 8) continue;
-      const f2 bb = cmul2(D[t], w512);
+      if (k2 > K2MAX) continue;
+      f2 wk = w512;
+      if (TWS && k2 > 0) wk = *reinterpret_cast<const f2*>(tb.tws + ((k2 - 1) * 16 + j) * 2);
+      const f2 bb = cmul2(D[t], wk);
       const f2 uvx = fma2(by(bb), f2{1.0f, -1.0f}, bx(S[t]));
       const f2 uvy = fma2(bx(bb), f2{-1.0f, 1.0f}, by(S[t]));
       pw[t] = fma2(uvx, uvx, uvy * uvy);
@@ -337,7 +354,7 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
 #pragma unroll
     for (int t = 0; t < G; ++t) {
       const int k2 = k0 + t;
-      if (k2 > 8) continue;
+      if (k2 > K2MAX) continue;
       const int kb = kc + 16 * k2;
       if (k2 < 8) {
         row[kb] = pw[t].x;
@@ -420,5 +437,15 @@ __device__ __forceinline__ f2 fe_w512(int j) {
   return f2{cs, sn};
 }
 __device__ __forceinline__ f2 fe_w512_lane(int j) { return fe_w512(fe_kcol(j)); }   // W512^k1 of the lane's column
+
+__device__ __forceinline__ void fe_init_tws(float* tws, int tid, int nthreads) {
+  for (int i = tid; i < 7 * 16; i += nthreads) {
+    const int k2 = i / 16 + 1, jj = i % 16;
+    float sn, cs;
+    sincospif(-(float)(fe_kcol(jj) + 16 * k2) / 256.0f, &sn, &cs);
+    tws[2 * i] = cs;
+    tws[2 * i + 1] = sn;
+  }
+}
 
 }  // namespace wk

@@ -46,7 +46,7 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
   const int g = lane >> 4, j = lane & 15;
 
   fe_init_tables<MODE_B>(smem, threadIdx.x, kFeBlock);
-  const FeTables tb = {smem + kWinOff, smem + kTwOff};
+  const FeTables tb = {smem + kWinOff, smem + kTwOff, nullptr};
   const f2 w512 = fe_w512_lane(j);
   // Frame slots: groups 0/1 (and 2/3) of a wave take frames 16 apart so their
   // pitch-17 transpose images fall in disjoint LDS banks.

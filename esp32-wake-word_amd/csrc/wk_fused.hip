@@ -41,6 +41,9 @@ __device__ unsigned long long g_wk_stamps[16][16];
 #endif
 
 constexpr int NBF = 4;               // clips per CNN batch
+#ifndef WK_FE_TWS
+#define WK_FE_TWS 1                  // real-FFT split with the combined twiddle table (fe_rest TWS)
+#endif
 #ifndef WK_DCT_EAGER
 #define WK_DCT_EAGER 1               // MFMA DCT of the next batch's clips between this batch's conv phases
 #endif
@@ -90,7 +93,8 @@ enum { kConvF32 = 0, kConvBf16 = 1, kConvBf16x3 = 2 };
 // Scratch power row for the one frame slot past the clip (frame 63): its lanes
 // still run the FFT so that the prefetch loads issued inside fe_rest execute.
 constexpr int kDummyRowOff = kImgEnd;
-constexpr int kFusedLds = kDummyRowOff + kPRow + 1;
+constexpr int kTwsOff = (kDummyRowOff + kPRow + 1) & ~1;   // combined split twiddles [7][16] f2 (8-byte aligned)
+constexpr int kFusedLds = kTwsOff + 7 * 16 * 2;
 static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 
 // kCtrlLFree + w (w = CNN wave 0..7): clips whose log-mel buffer CNN wave w
@@ -181,7 +185,7 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   float* L1 = smem + kL1Off;
   unsigned* ctrl = reinterpret_cast<unsigned*>(smem + kCtrlOff);
   const int g = lane >> 4, j = lane & 15;
-  const FeTables tb = {smem + kWinOff, smem + kTwOff};
+  const FeTables tb = {smem + kWinOff, smem + kTwOff, WK_FE_TWS ? smem + kTwsOff : nullptr};
   const f2 w512 = fe_w512_lane(j);
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);
   const int fw = wave;   // frame slot of this wave (moving the edge frames to other waves measured neutral)
@@ -248,7 +252,7 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
         WK_STAMP(9);
       }
       float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
-      fe_rest<true>(a, j, lane, row, tb, w512, 0, pf_part WK_SP_ARG);
+      fe_rest<true, decltype(pf_part), (bool)WK_FE_TWS>(a, j, lane, row, tb, w512, 0, pf_part WK_SP_ARG);
     }
     if (exp_flags & 4) __builtin_amdgcn_s_setprio(1); else if (exp_flags & 8) __builtin_amdgcn_s_setprio(0);
     role_sync(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
@@ -646,7 +650,8 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   fe_init_tables<true>(smem, tid, kFusedBlock);
-  for (int i = tid; i < kFusedLds - kGOff; i += kFusedBlock) smem[kGOff + i] = 0.0f;  // ctrl, guards, pads
+  if (WK_FE_TWS) fe_init_tws(smem + kTwsOff, tid, kFusedBlock);
+  for (int i = tid; i < kTwsOff - kGOff; i += kFusedBlock) smem[kGOff + i] = 0.0f;  // ctrl, guards, pads
   __syncthreads();
   const int64_t n_mine = batch > (int64_t)blockIdx.x ? (batch - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   if (wave < 8) {
