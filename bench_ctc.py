@@ -3,7 +3,8 @@
 B utterances of 3 s (48,000 samples, T = 301 frames at hop 160), synthetic
 (device generator), seeded GRU_CTC_Model weights (the reference ships none),
 fixed V.  One step = log-mel front-end + encoder + 2-layer BiGRU + output
-layer + log_softmax/argmax + greedy decode, inputs resident in HBM.  Prints
+layer + argmax + greedy decode, inputs resident in HBM and the token
+sequences left there (CTCModel.decode; forward() adds the host list form).  Prints
 one JSON line with utterances/s, the per-stage split, and the torch-CPU
 oracle timed on a bounded sample of the same workload."""
 import argparse
@@ -45,7 +46,7 @@ def main():
         ev[0].record()
         f = g.features(audio, n_samples=n)
         ev[1].record()
-        g.forward(f)
+        g.decode(f)   # tokens + lengths stay in HBM (the host list form is forward())
         ev[2].record()
         torch.cuda.synchronize()
         t_fe += ev[0].elapsed_time(ev[1])

@@ -24,6 +24,9 @@
 //                         pre-activations through LDS, gates + state update.
 //   ctc_argmax_kernel     one wave per row: bias, max/argmax (first index),
 //                         log-sum-exp, optional log_softmax output.
+//   ctc_argmax_only_kernel  the same argmax when no log-probs are asked for:
+//                         persistent, bias in LDS, a row's loads issued a row
+//                         ahead, no exp.
 //   ctc_greedy_kernel     one thread per utterance: drop blanks, collapse repeats.
 #include <stdlib.h>
 #include <string.h>
@@ -400,6 +403,65 @@ __global__ __launch_bounds__(256) void ctc_argmax_kernel(const LT* __restrict__ 
   if (lane == 0) best[r] = arg;
 }
 
+// Argmax only (no log_softmax requested: the greedy decode needs just the
+// index -- log_softmax is monotonic per row, ctc.py:455 takes torch.max of
+// it).  Persistent: the bias row sits in LDS once per block; each wave walks
+// rows r = wave, wave + n_waves, ...; a row's 16-byte chunks are loaded up
+// front (kArgChunks per lane), so a row costs one memory round trip, and the
+// next row's loads are issued before the current row is reduced.  No exp.
+constexpr int kArgChunks = 8;   // 16-byte chunks per lane per row
+template <typename LT>
+__global__ __launch_bounds__(256) void ctc_argmax_only_kernel(const LT* __restrict__ logits,
+                                                              const float* __restrict__ bias, int64_t rows, int V,
+                                                              int* __restrict__ best) {
+  constexpr int NV = Vec<LT>::N;
+  extern __shared__ float sb[];   // [V] bias
+  for (int v = threadIdx.x; v < V; v += blockDim.x) sb[v] = bias[v];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int nc = V / NV;   // chunks per row (host checks V % NV == 0 and nc <= 64 * kArgChunks)
+  auto load_row = [&](int64_t r, uint4 (&buf)[kArgChunks]) {
+    const uint4* x = reinterpret_cast<const uint4*>(logits + r * V);
+#pragma unroll
+    for (int k = 0; k < kArgChunks; ++k) {
+      const int c = lane + 64 * k;
+      buf[k] = c < nc ? x[c] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  uint4 cur[kArgChunks];
+  if (r < rows) load_row(r, cur);
+  for (; r < rows; r += nw) {
+    uint4 nxt[kArgChunks];
+    if (r + nw < rows) load_row(r + nw, nxt);
+    float mx = -INFINITY;
+    int arg = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < kArgChunks; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nc) {
+        LT e[NV];
+        *reinterpret_cast<uint4*>(e) = cur[k];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {   // ascending index: strict > keeps the first maximum
+          const float y = (float)e[i] + sb[c * NV + i];
+          if (y > mx) { mx = y; arg = c * NV + i; }
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const float om = __shfl_xor(mx, m, 64);
+      const int oa = __shfl_xor(arg, m, 64);
+      if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+    }
+    if (lane == 0) best[r] = arg;
+#pragma unroll
+    for (int k = 0; k < kArgChunks; ++k) cur[k] = nxt[k];
+  }
+}
+
 __global__ void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T, int* __restrict__ tokens,
                                   int* __restrict__ lengths) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -744,7 +806,16 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
     wk_status s = f16 ? gemm_nt(c->blas, rows, V, 2 * H, c->y1h, c->out_w16, c->logits16, true, true)
                       : gemm_nt(c->blas, rows, V, 2 * H, c->y1, c->out_w, c->logits, false);
     if (s != WK_OK) return s;
-    if (f16)   // fp16 logits: half the HBM traffic of the [rows][V] intermediate
+    const int nv = f16 ? Vec<__half>::N : Vec<float>::N;
+    const bool arg_only = !d_log_probs && V % nv == 0 && V / nv <= 64 * kArgChunks && V <= 16384;
+    const unsigned ag = (unsigned)((rows + 3) / 4 < 8 * c->n_cu ? (rows + 3) / 4 : 8 * c->n_cu);
+    if (arg_only && f16)
+      hipLaunchKernelGGL(ctc_argmax_only_kernel<__half>, dim3(ag), dim3(256), V * sizeof(float), st, c->logits16,
+                         c->out_b, rows, V, c->best);
+    else if (arg_only)
+      hipLaunchKernelGGL(ctc_argmax_only_kernel<float>, dim3(ag), dim3(256), V * sizeof(float), st, c->logits,
+                         c->out_b, rows, V, c->best);
+    else if (f16)   // fp16 logits: half the HBM traffic of the [rows][V] intermediate
       hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits16,
                          c->out_b, rows, V, d_log_probs, c->best);
     else

@@ -57,8 +57,11 @@ class CTCModel:
                                     self._stream(torch)), "wk_ctc_features")
         return out
 
-    def forward(self, feats, return_log_probs: bool = False):
-        """(B, T, 80) -> token id lists (greedy CTC), and (B, T, V) log-probs if asked."""
+    def decode(self, feats, return_log_probs: bool = False):
+        """(B, T, 80) -> device tensors, stream-ordered, no host sync: tokens
+        (B, T) int32 (row b's first lengths[b] entries are its greedy CTC
+        sequence, the rest -1), lengths (B,) int32, and (B, T, V) log-probs
+        if asked (else None)."""
         import torch
         f = torch.as_tensor(feats, dtype=torch.float32).to(f"cuda:{self.device}").contiguous()
         B, T, _ = f.shape
@@ -68,8 +71,14 @@ class CTCModel:
         check(lib().wk_ctc_forward(self._h, C.c_void_p(f.data_ptr()), B, T,
                                    C.c_void_p(lp.data_ptr()) if lp is not None else None, C.c_void_p(tok.data_ptr()),
                                    C.c_void_p(ln.data_ptr()), self._stream(torch)), "wk_ctc_forward")
+        return tok, ln, lp
+
+    def forward(self, feats, return_log_probs: bool = False):
+        """(B, T, 80) -> token id lists (greedy CTC, decode_predictions'
+        output form), and (B, T, V) log-probs if asked."""
+        tok, ln, lp = self.decode(feats, return_log_probs)
         tok, ln = tok.cpu().numpy(), ln.cpu().numpy()
-        seqs = [tok[b, :ln[b]].tolist() for b in range(B)]
+        seqs = [tok[b, :ln[b]].tolist() for b in range(tok.shape[0])]
         return (seqs, lp) if return_log_probs else seqs
 
     def transcribe(self, audio, n_samples: int = MAX_AUDIO_SAMPLES) -> List[List[int]]:

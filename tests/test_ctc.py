@@ -86,6 +86,21 @@ def test_ctc_end_to_end_and_bad_args(ctc):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_ctc_argmax_only_path_matches_log_prob_path(ctc, precision):
+    """Without log-probs the output layer takes the argmax-only kernel (no
+    log-sum-exp): its tokens must equal the log_softmax path's exactly (both
+    take the first maximum of logit + bias)."""
+    import wakeword
+    m, _ = ctc
+    g = wakeword.CTCModel(CO.flat_weights(m), V, precision=precision)
+    feats = CO.features(torch.from_numpy(O.synth_clips(7, 0, 33, 48000)))
+    seqs_lp, _ = g.forward(feats, return_log_probs=True)
+    seqs = g.forward(feats)
+    assert seqs == seqs_lp
+
+
+@pytest.mark.gpu
 def test_ctc_fp16_gemm_mode(ctc):
     """precision='fp16' (config 5): GEMM operands in fp16, fp32 accumulation and
     recurrence -- looser log-prob bound, same decisions on confident frames."""
