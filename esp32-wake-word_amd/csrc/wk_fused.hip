@@ -407,9 +407,12 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     for (int s = 0; s < 12; ++s) w3b[s] = frag_bf(kPbW3 + (cw * 12 + s) * 256);
   }
 #ifndef WK_W3_RESIDENT
-#define WK_W3_RESIDENT 1   // fp32 conv3 taps in VGPRs across batches (1; measured +5 %) or re-read from L2 per pass (0)
+#define WK_W3_RESIDENT 1   // fp32 conv3 taps: in VGPRs across batches (1), re-read from L2 per pass (0), or loaded
+                           // once per batch as conv2 ends (2: no DCT-time spills, but 5 % slower than 1 with its
+                           // 18 spilled VGPRs, which are reloaded from L1 at the sync points)
 #endif
-  if constexpr (CM == kConvF32 && WK_W3_RESIDENT) {
+  constexpr bool kW3Batch = CM == kConvF32 && WK_W3_RESIDENT == 2;
+  if constexpr (CM == kConvF32 && WK_W3_RESIDENT == 1) {
 #pragma unroll
     for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
   }
@@ -544,9 +547,13 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
         epi_wino_pool<F2_CIP, I2_TP, 15>(m, F2, co0, cl, 0, lane);
       }
     }
+    if constexpr (kW3Batch) {
+#pragma unroll
+      for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
+    }
     WK_STAMP(3);
     role_sync(ctrl, kCtrlCnnBar, gen, lane);
-    try_eager(b);
+    if (!kW3Batch) try_eager(b);   // (w3 is live from here to the end of conv3)
     WK_STAMP(4);
 
     // conv3: co tile cw, the 4 clips; GAP -> G[128][4].
