@@ -367,7 +367,10 @@ __device__ __forceinline__ void dct_cmvn_clip(const float* __restrict__ lbuf, in
 // ---------------------------------------------------------------------------
 // CNN role (waves 8-15): batches of NBF clips from the conv1 image.
 // ---------------------------------------------------------------------------
-template <int CM>   // kConvF32 / kConvBf16 / kConvBf16x3
+// FEATS: the launch also writes the CMVN'd features (parity dumps).  A
+// template flag rather than a null test, so the product kernel carries no
+// feature-store code (its address registers pushed the fp32 build to spill).
+template <int CM, bool FEATS>   // kConvF32 / kConvBf16 / kConvBf16x3
 __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ pk, const uint16_t* __restrict__ pkb,
                                          int64_t n_mine, float* __restrict__ logits, float* __restrict__ feats_out,
                                          int cw, int lane, int exp_flags) {
@@ -423,7 +426,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   signal_set(ctrl, kCtrlLFree + cw, cw < NBF ? (unsigned)cw : 0xFFFFFFFFu, lane);
   bool eager_done = false;
   auto dct_clip = [&](int64_t i, int slot) {
-    float* fo = feats_out ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) : nullptr;
+    float* fo = FEATS ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) : nullptr;
     dct_cmvn_clip<CM>(i & 1 ? L1 : L, slot, F0, B0, X0, fo, lane);
     signal_set(ctrl, kCtrlLFree + cw, (unsigned)(i + NBF), lane);
   };
@@ -646,7 +649,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   WK_STAMP_FLUSH(8 + cw);
 }
 
-template <typename T, int CM>
+template <typename T, int CM, bool FEATS>
 __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __restrict__ audio, int64_t batch,
                                                                  int64_t clip_stride, const float* __restrict__ wts,
                                                                  const uint16_t* __restrict__ wbf,
@@ -667,7 +670,7 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
 #endif
   } else {
 #ifndef WK_EXPERIMENT_NO_CNN
-    if (!(exp_flags & 1)) cnn_role<CM>(smem, wts, wbf, n_mine, logits, feats_out, wave - 8, lane, exp_flags);
+    if (!(exp_flags & 1)) cnn_role<CM, FEATS>(smem, wts, wbf, n_mine, logits, feats_out, wave - 8, lane, exp_flags);
 #endif
   }
 }
@@ -694,9 +697,15 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
   const int grid = (int)(batch < grid_cap ? batch : grid_cap);
   const dim3 g(grid), blk(kFusedBlock);
   if (conv_mode != kConvF32 && !wbf) return hipErrorInvalidValue;
-#define WK_FUSED_LAUNCH(T, CM)                                                                          \
-  hipLaunchKernelGGL((wk_fused_kernel<T, CM>), g, blk, 0, stream, (const T*)audio, batch, clip_stride, w, wbf, \
-                     logits, feats_or_null, exp_flags)
+#define WK_FUSED_LAUNCH(T, CM)                                                                              \
+  do {                                                                                                         \
+    if (feats_or_null)                                                                                         \
+      hipLaunchKernelGGL((wk_fused_kernel<T, CM, true>), g, blk, 0, stream, (const T*)audio, batch, clip_stride, \
+                         w, wbf, logits, feats_or_null, exp_flags);                                            \
+    else                                                                                                       \
+      hipLaunchKernelGGL((wk_fused_kernel<T, CM, false>), g, blk, 0, stream, (const T*)audio, batch,            \
+                         clip_stride, w, wbf, logits, nullptr, exp_flags);                                     \
+  } while (0)
   if (i16) {
     if (conv_mode == kConvBf16) WK_FUSED_LAUNCH(int16_t, kConvBf16);
     else if (conv_mode == kConvBf16x3) WK_FUSED_LAUNCH(int16_t, kConvBf16x3);

@@ -39,7 +39,7 @@ case "$BARGS" in *bf16x3*) BF=2; TF=hbm_traffic_bf16x3.json ;; *bf16*) BF=1; TF=
 python3 - "$OUT/${TAG}_pmc.json" "$OUT/$TF" "$TAG" "$BF" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
-kname = f"wk_fused_kernel<float, {sys.argv[4]}>"
+kname = f"wk_fused_kernel<float, {sys.argv[4]}, false>"
 k = next(v for n, v in d.items() if n.startswith(kname))
 B = 65536   # bench default batch (tools/profile_pmc.sh runs the default bench)
 rd, wr = k["hbm_read_bytes_corrected"], k.get("hbm_write_bytes", 0.0)
