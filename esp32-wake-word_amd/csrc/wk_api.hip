@@ -246,6 +246,17 @@ wk_status wk_normalize(const float* d_in, float* d_out, int64_t batch, int32_t n
   return e == hipSuccess ? WK_OK : hip_fail(e, "normalize launch");
 }
 
+wk_status wk_device_cmvn(const void* d_frames, int32_t dtype, int64_t n_frames, int8_t* d_out_i8,
+                         float* d_feats_or_null, void* stream) {
+  if (n_frames < 0 || (dtype != WK_DTYPE_I8 && dtype != WK_DTYPE_F32)) return invalid("wk_device_cmvn: bad args");
+  if (!d_out_i8 && !d_feats_or_null) return invalid("wk_device_cmvn: no output");
+  const int64_t n_windows = n_frames >= 63 ? n_frames - 62 : 0;
+  if (n_windows > 0 && !d_frames) return invalid("wk_device_cmvn: null frames");
+  hipError_t e = wk::launch_device_cmvn(d_frames, dtype == WK_DTYPE_I8, n_windows, d_out_i8, d_feats_or_null,
+                                        (hipStream_t)stream);
+  return e == hipSuccess ? WK_OK : hip_fail(e, "device_cmvn launch");
+}
+
 // ---------------------------------------------------------------------------
 // mfcc.h compatibility shims (main/esp_mfcc/mfcc.h:10-17, mfcc.c:431-563).
 // ---------------------------------------------------------------------------

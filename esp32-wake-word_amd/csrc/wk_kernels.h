@@ -58,6 +58,9 @@ void quantize_int8_weights(const float* w, int8_t* q);
 hipError_t launch_synth(uint32_t seed, int64_t first, int64_t count, int n, float* out, hipStream_t stream);
 hipError_t launch_normalize(const float* in, float* out, int64_t batch, int n_coef, int n_time, int method,
                             hipStream_t stream);
+// The firmware's per-window CMVN over an MFCC frame stream (wk_device_cmvn).
+hipError_t launch_device_cmvn(const void* frames, bool int8_in, int64_t n_windows, int8_t* out_i8, float* out_f,
+                              hipStream_t stream);
 
 // Offsets (floats) of each tensor inside the packed weight blob.
 constexpr int kOffW1 = 0;                       // conv_layers.0.weight [32][13][3]

@@ -78,9 +78,64 @@ __global__ void wk_normalize_kernel(const float* __restrict__ in, float* __restr
   }
 }
 
+// The firmware's int8 MFCC quantisation (record_task, esp_wake_word_detector.cpp:128-131):
+// lroundf (half away from zero) then saturate to int8.
+__device__ __forceinline__ float device_q(float v) { return fminf(fmaxf(__builtin_roundf(v), -128.0f), 127.0f); }
+__device__ __forceinline__ float device_q(int8_t v) { return (float)v; }
+
+// The firmware's per-window CMVN (detect_task, esp_wake_word_detector.cpp:179-211) over
+// a stream of MFCC frames [n][13] (frame-major, as write_one_frame_mfcc_to_buffer
+// stores them): window w is frames w .. w+62, oldest first (read_whole_mfcc_buffer,
+// :21-29).  Per coefficient: mean over the 63 frames, POPULATION std (/63),
+// (v - mean) / (std + 1e-8), lroundf, saturate to int8.  One thread per (window,
+// coefficient), summing frame 0 .. 62 in the firmware's order with no FMA
+// contraction, so the int8 results are bit-identical to the C loops (the sums of
+// int8 values are exact in fp32; the variance sum, division and sqrt are
+// IEEE-rounded in the same order).  Outputs: the device's int8 buffer [w][63][13]
+// and/or the same values as float features [w][13][63] (wk_cnn's layout: the
+// esp-dl model reads the frame-major buffer as its NWC input).
+template <typename T>
+__global__ void wk_device_cmvn_kernel(const T* __restrict__ frames, int64_t n_windows, int8_t* __restrict__ out_i8,
+                                      float* __restrict__ out_f) {
+#pragma clang fp contract(off)
+  const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (idx >= n_windows * 13) return;
+  const int64_t w = idx / 13;
+  const int dim = (int)(idx - w * 13);
+  const T* x = frames + w * 13 + dim;
+  float sum = 0.0f;
+  for (int f = 0; f < 63; ++f) sum += device_q(x[f * 13]);
+  const float mean = sum / 63.0f;
+  float var = 0.0f;
+  for (int f = 0; f < 63; ++f) {
+    const float d = device_q(x[f * 13]) - mean;
+    var += d * d;
+  }
+  const float sd = sqrtf(var / 63.0f);
+  for (int f = 0; f < 63; ++f) {
+    const float q = fminf(fmaxf(__builtin_roundf((device_q(x[f * 13]) - mean) / (sd + 1e-8f)), -128.0f), 127.0f);
+    if (out_i8) out_i8[(w * 63 + f) * 13 + dim] = (int8_t)q;
+    if (out_f) out_f[(w * 13 + dim) * 63 + f] = q;
+  }
+}
+
 }  // namespace
 
 namespace wk {
+
+hipError_t launch_device_cmvn(const void* frames, bool int8_in, int64_t n_windows, int8_t* out_i8, float* out_f,
+                              hipStream_t stream) {
+  if (n_windows <= 0) return hipSuccess;
+  const int64_t threads = n_windows * 13;
+  const unsigned blocks = (unsigned)((threads + 255) / 256);
+  if (int8_in)
+    hipLaunchKernelGGL(wk_device_cmvn_kernel<int8_t>, dim3(blocks), dim3(256), 0, stream, (const int8_t*)frames,
+                       n_windows, out_i8, out_f);
+  else
+    hipLaunchKernelGGL(wk_device_cmvn_kernel<float>, dim3(blocks), dim3(256), 0, stream, (const float*)frames,
+                       n_windows, out_i8, out_f);
+  return hipGetLastError();
+}
 
 hipError_t launch_synth(uint32_t seed, int64_t first, int64_t count, int n, float* out, hipStream_t stream) {
   const int64_t total = count * (int64_t)n;

@@ -8,7 +8,8 @@ from ._lib import WakewordError, lib  # noqa: F401
 from .api import (KWSModel, detect, extract_mfcc, load_onnx, load_wav, mfcc, normalize_mfcc, pack_weights,  # noqa: F401
                   pad_audio, synth_clips)
 from .onnx_reader import read_onnx, xiaoa_state_dict  # noqa: F401
-from .stream import DecisionRule, StreamingDetector, Window  # noqa: F401
+from .stream import (DecisionRule, DeviceDetector, FrameDecisionLoop, FrameWindow, StreamingDetector,  # noqa: F401
+                     Window, device_cmvn)
 from .ctc import CTCModel  # noqa: F401
 from . import wav  # noqa: F401
 

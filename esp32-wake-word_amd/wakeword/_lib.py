@@ -17,6 +17,7 @@ WK_MODE_TORCHAUDIO_CMVN = 0
 WK_MODE_ESP_MFCC = 1
 WK_DTYPE_F32 = 0
 WK_DTYPE_I16 = 1
+WK_DTYPE_I8 = 2
 WK_PREC_FP32 = 0
 WK_PREC_BF16 = 1
 WK_PREC_INT8 = 2
@@ -28,7 +29,7 @@ EXPORTS = ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_syn
            "wk_status_string", "wk_last_error", "wk_abi_version", "extract_mfcc", "free_mfcc",
            "analyze_mfcc_range", "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push",
            "wk_ctc_num_weights", "wk_ctc_create", "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward",
-           "wk_wav_read", "wk_wav_load_batch", "wk_augment", "flow_extract_mfcc_single_frame")
+           "wk_wav_read", "wk_wav_load_batch", "wk_augment", "flow_extract_mfcc_single_frame", "wk_device_cmvn")
 
 
 class WkConfig(C.Structure):
@@ -86,10 +87,11 @@ def _declare(L):
     L.wk_wav_read.argtypes = [C.c_char_p, vp, i32, C.POINTER(WkWavInfo)]
     L.wk_wav_load_batch.argtypes = [C.POINTER(C.c_char_p), i32, i32, C.c_float, u32, vp, vp]
     L.wk_augment.argtypes = [vp, i32, C.c_float, C.c_float, C.c_float, u32, vp, i32]
+    L.wk_device_cmvn.argtypes = [vp, i32, i64, vp, vp, vp]
     for name in ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_synth_clips", "wk_normalize",
                  "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push", "wk_ctc_create",
                  "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward", "wk_wav_read", "wk_wav_load_batch",
-                 "wk_augment"):
+                 "wk_augment", "wk_device_cmvn"):
         getattr(L, name).restype = i32
 
 

@@ -92,3 +92,111 @@ class StreamingDetector:
             self.close()
         except Exception:
             pass
+
+
+# ---------------------------------------------------------------------------
+# The firmware's detector over an MFCC frame stream (esp_wake_word_detector.cpp)
+# ---------------------------------------------------------------------------
+FRAME_WIN = 63           # frames per window (MFCC_LEN = 13*63, :3)
+N_COEF = 13
+
+
+def device_cmvn(frames, device: int = 0):
+    """wk_device_cmvn on an MFCC frame stream [n][13] (int8 as the firmware
+    stores it, or float MFCC quantised first as record_task :128-131 does):
+    returns (int8 [n-62][63][13] -- the firmware's mfcc_cmvn_buffer per window --,
+    float [n-62][13][63] -- the same values in wk_cnn's feature layout)."""
+    import torch
+    x = frames
+    if isinstance(x, np.ndarray):
+        x = torch.from_numpy(np.ascontiguousarray(x))
+    is_i8 = x.dtype == torch.int8
+    x = x.to(device=f"cuda:{device}", dtype=torch.int8 if is_i8 else torch.float32).contiguous()
+    if x.dim() != 2 or x.shape[1] != N_COEF:
+        raise ValueError(f"expected frames (n, 13), got {tuple(x.shape)}")
+    nw = max(x.shape[0] - (FRAME_WIN - 1), 0)
+    q = torch.empty((nw, FRAME_WIN, N_COEF), dtype=torch.int8, device=x.device)
+    f = torch.empty((nw, N_COEF, FRAME_WIN), dtype=torch.float32, device=x.device)
+    st = torch.cuda.current_stream(x.device)
+    check(lib().wk_device_cmvn(C.c_void_p(x.data_ptr()), _lib.WK_DTYPE_I8 if is_i8 else _lib.WK_DTYPE_F32,
+                               x.shape[0], C.c_void_p(q.data_ptr()), C.c_void_p(f.data_ptr()),
+                               C.c_void_p(st.cuda_stream)), "wk_device_cmvn")
+    return q, f
+
+
+@dataclass
+class FrameWindow:
+    end: int          # index (frames since start) of the window's newest frame
+    logit: float      # model output (int8 model: raw * 2^-3, as the firmware dequantises it, :226-227)
+    pct: float        # sigmoid * 100 (:228)
+    detected: bool
+
+
+class FrameDecisionLoop:
+    """detect_task's control flow (esp_wake_word_detector.cpp:171-258) in the
+    frame domain (host logic, testable without a GPU).  The window ending at
+    frame e is scored once 64 frames were written since the last reset
+    (shared_counter == 64, :38-44,141 -- the 64th frame overwrites the first, so
+    the window is the newest 63); sigmoid*100 >= threshold fires (:245); the
+    task then sleeps 5 s = `deaf_frames` frames of 20 ms (:248) and clears the
+    ring (:251-256), so the next window needs 64 frames written after that.
+    (The firmware also runs one extra inference on the just-cleared buffer
+    when it wakes, from the notification left pending during the sleep; it is
+    not modelled.)"""
+
+    def __init__(self, threshold_pct: float = 80.0, deaf_frames: int = 250):
+        self.threshold = np.float32(threshold_pct)
+        self.deaf = deaf_frames
+        self.reset_at = 0          # first frame written after the last reset
+
+    def scored(self, e: int) -> bool:
+        return e - self.reset_at >= FRAME_WIN
+
+    def __call__(self, e: int, logit: float) -> FrameWindow:
+        x = np.float32(logit)
+        pct = np.float32(1.0) / (np.float32(1.0) + np.exp(-x)) * np.float32(100.0)
+        fire = bool(pct >= self.threshold)
+        if fire:
+            self.reset_at = e + self.deaf + 1
+        return FrameWindow(e, float(x), float(pct), fire)
+
+
+class DeviceDetector:
+    """The firmware's wake-word loop on an MFCC frame stream, on the GPU:
+    push(frames [n][13]) -> the windows it scored.  Each push runs
+    wk_device_cmvn over the new windows and the model (normally a
+    precision='int8' KWSModel: the device's esp-dl int8 network) in one batch;
+    the decision loop then walks them in order.  The MFCC frames themselves come
+    from esp-dl's dl::audio::MFCC on the device (a third-party library absent
+    here): the caller supplies them, int8 or float."""
+
+    def __init__(self, model, threshold_pct: float = 80.0, refractory_s: float = 5.0, frame_s: float = 0.02):
+        self._model = model
+        self.loop = FrameDecisionLoop(threshold_pct, int(round(refractory_s / frame_s)))
+        self._tail = None          # the last <= 62 frames of earlier pushes
+        self._next = 0             # index of the next frame to arrive
+
+    def push(self, frames) -> List[FrameWindow]:
+        f = np.asarray(frames)
+        if f.ndim != 2 or f.shape[1] != N_COEF:
+            raise ValueError(f"expected frames (n, 13), got {f.shape}")
+        if f.dtype != np.int8:
+            f = f.astype(np.float32)
+        if self._tail is not None and self._tail.dtype != f.dtype:   # int8 frames as floats quantise to themselves
+            f, self._tail = f.astype(np.float32), self._tail.astype(np.float32)
+        cat = f if self._tail is None else np.concatenate([self._tail, f])
+        first = self._next - (0 if self._tail is None else self._tail.shape[0])   # frame index of cat[0]
+        self._next += f.shape[0]
+        self._tail = cat[-(FRAME_WIN - 1):].copy()
+        out: List[FrameWindow] = []
+        if cat.shape[0] < FRAME_WIN:
+            return out
+        ends = np.arange(first + FRAME_WIN - 1, first + cat.shape[0])
+        if not any(self.loop.scored(int(e)) for e in ends):   # (reset_at only grows during the walk)
+            return out
+        _, feats = device_cmvn(cat, self._model.device)
+        logits = self._model(feats).reshape(-1).cpu().numpy()
+        for e, lg in zip(ends, logits):
+            if self.loop.scored(int(e)):
+                out.append(self.loop(int(e), float(lg)))
+        return out

@@ -43,7 +43,7 @@ typedef enum {
   WK_MODE_ESP_MFCC = 1         /* mode A: esp_mfcc/mfcc.c:431-527, out [n_frames][13]     */
 } wk_mode;
 
-typedef enum { WK_DTYPE_F32 = 0, WK_DTYPE_I16 = 1 } wk_dtype;   /* audio sample type */
+typedef enum { WK_DTYPE_F32 = 0, WK_DTYPE_I16 = 1, WK_DTYPE_I8 = 2 } wk_dtype;   /* sample / frame type */
 /* CNN arithmetic.  FP32 = fp32 MFMA.  BF16 = bf16 convolutions (SURVEY
  * config 4), fp32 front-end/classifier.  INT8 = the device's esp-dl int8
  * network (power-of-2 per-tensor exponents of ml_models/xiaoa.info,
@@ -131,6 +131,26 @@ wk_status wk_stream_destroy(wk_stream* s);
 wk_status wk_stream_reset(wk_stream* s);   /* forget history (post-detection reset, detector.cpp:249-256) */
 wk_status wk_stream_push(wk_stream* s, const float* host_samples, int64_t n, float* out_logits, int64_t* out_end,
                          int32_t max_out, int32_t* n_out);
+
+/* ---- The firmware's detector over an MFCC frame stream --
+ * esp_wake_word_detector.cpp keeps the last 63 int8 MFCC frames of 13
+ * coefficients (record_task :128-134 quantises each 20 ms frame with lroundf +
+ * saturation; write_one_frame_mfcc_to_buffer / read_whole_mfcc_buffer :21-48
+ * hand the detector the 63 newest frames, oldest first) and, per window,
+ * applies its own CMVN (detect_task :179-211: mean and POPULATION std over the 63
+ * frames, (v - mean) / (std + 1e-8), lroundf, saturate) before the int8 model.
+ * wk_device_cmvn runs that CMVN for every window of a frame stream: d_frames
+ * [n_frames][13] (WK_DTYPE_I8 = the firmware's int8 frames, or WK_DTYPE_F32 =
+ * float MFCC frames, quantised first as record_task does); window w = frames
+ * w .. w+62, n_frames - 62 windows (none if n_frames < 63).  Outputs (either may
+ * be NULL, not both): d_out_i8 [w][63][13] -- the firmware's mfcc_cmvn_buffer --
+ * and d_feats_or_null [w][13][63], the same integer values as floats in wk_cnn's
+ * layout (feed it to a WK_PREC_INT8 handle for the device's int8 network:
+ * dl::TensorBase::assign from exponent 0 to the input exponent -4 is x16 with
+ * saturation, which is what WK_PREC_INT8 applies to its float input).
+ * Bit-identical to the firmware's C loops (same fp32 summation order). */
+wk_status wk_device_cmvn(const void* d_frames, int32_t dtype, int64_t n_frames, int8_t* d_out_i8,
+                         float* d_feats_or_null, void* stream);
 
 /* ---- CTC head (ml_models/ctc.py) -------------------------
  * GRU_CTC_Model (ctc.py:119-152) + its log-mel front-end (ctc.py:82-107) +

@@ -340,3 +340,63 @@ def quantize_input(feats: np.ndarray) -> np.ndarray:
     """TensorBase::assign float -> int8 at exp -4 (round half away from zero, saturate)."""
     v = np.asarray(feats, np.float64) * 16.0
     return np.clip(np.sign(v) * np.floor(np.abs(v) + 0.5), -128, 127).astype(np.int64)
+
+
+# --------------------------------------------------------------------------
+# The firmware's detector over an MFCC frame stream (SURVEY 8(f) item 1):
+# main/esp_wake_word_detector/src/esp_wake_word_detector.cpp.  fp32 numpy ops
+# are each IEEE-rounded, in the firmware's loop order, so the int8 results are
+# the C loops' results bit for bit.
+# --------------------------------------------------------------------------
+def device_quantize_frames(mfcc: np.ndarray) -> np.ndarray:
+    """record_task :128-131: (int32_t)lroundf(v), saturated to int8."""
+    v = np.asarray(mfcc, np.float32).astype(np.float64)
+    return np.clip(np.sign(v) * np.floor(np.abs(v) + 0.5), -128, 127).astype(np.int8)
+
+
+def device_cmvn(frames: np.ndarray) -> np.ndarray:
+    """detect_task :179-211 for every 63-frame window of an int8 frame stream
+    [n][13] (window w = frames w..w+62, read_whole_mfcc_buffer order :21-29):
+    mean, population std (/63), (v - mean) / (std + 1e-8), lroundf, saturate.
+    Returns int8 [n-62][63][13] (the firmware's mfcc_cmvn_buffer)."""
+    f = np.asarray(frames, np.int8).astype(np.float32)
+    n = f.shape[0]
+    if n < 63:
+        return np.zeros((0, 63, 13), np.int8)
+    win = np.lib.stride_tricks.sliding_window_view(f, (63, 13))[:, 0]   # (W, 63, 13)
+    s = np.zeros((win.shape[0], 13), np.float32)
+    for t in range(63):
+        s = s + win[:, t]
+    mean = s / np.float32(63.0)
+    var = np.zeros_like(s)
+    for t in range(63):
+        d = win[:, t] - mean
+        var = var + d * d
+    sd = np.sqrt(var / np.float32(63.0))
+    nrm = (win - mean[:, None, :]) / (sd[:, None, :] + np.float32(1e-8))
+    return device_quantize_frames(nrm)
+
+
+def device_decisions(n_frames: int, logits: np.ndarray, threshold_pct: float = 80.0, deaf_frames: int = 250):
+    """detect_task's control flow (:171-258) in the frame domain, as a plain loop:
+    the window ending at frame e (frames e-62..e) is scored once 64 frames were
+    written since the last reset (shared_counter == 64, :38-44,141); a score
+    sigmoid(x)*100 >= 80 (:228,245) fires, the task sleeps 5 s (250 frames of 20
+    ms, :248) and then clears the buffer (:251-256).  logits[e - 62] is the
+    window ending at frame e.  Returns (end_frame, detected) of every scored window."""
+    out, reset = [], 0
+    e = 62
+    while e < n_frames:
+        if e - reset < 63:
+            e += 1
+            continue
+        x = np.float32(logits[e - 62])
+        pct = np.float32(1.0) / (np.float32(1.0) + np.exp(-x)) * np.float32(100.0)
+        fire = bool(pct >= np.float32(threshold_pct))
+        out.append((e, fire))
+        if fire:
+            reset = e + deaf_frames + 1
+            e = reset
+            continue
+        e += 1
+    return out
