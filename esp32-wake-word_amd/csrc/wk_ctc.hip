@@ -7,14 +7,13 @@
 //         -> greedy CTC decode (ctc.py:453-471)
 //
 // Kernels:
-//   ctc_frames_kernel     reflect-padded frames x periodic Hann(400) -> [rows][400];
-//                         the 400-point DFT (201 bins) is a GEMM against the
-//                         [402][400] cos/-sin matrix (rocBLAS, fp32);
-//   ctc_power_mel_kernel  power, HTK mel (CSR weights), ln(+1e-8), one wave per frame.
+//   ctc_logmel_fft_kernel reflect-padded frames x periodic Hann(400) -> 400-point
+//                         real DFT as a 20 x 20 four-step FFT in registers + LDS
+//                         -> power -> HTK mel (CSR weights) -> ln(+1e-8), fused.
 //   ctc_zscore_kernel     one block per utterance, two-pass mean / unbiased std.
 //   ctc_encoder_kernel    one wave per frame row, weights in LDS, LayerNorm via
 //                         DPP wave sums.
-//   GEMMs (the DFT, input projections of both GRU directions, the output
+//   GEMMs (input projections of both GRU directions, the output
 //                         layer): plain library GEMMs (rocblas_gemm_ex; fp16
 //                         operands with fp32 accumulation when precision = 1).
 //   ctc_gru_kernel        persistent recurrence: one 768-thread block per
@@ -49,49 +48,139 @@ constexpr int kNfft = 400, kHop = 160, kBins = kNfft / 2 + 1, kMels = 80, kH = 1
 // ---------------------------------------------------------------------------
 // X1: log-mel
 // ---------------------------------------------------------------------------
-// Frame t of utterance b covers positions [t*160, t*160 + 400) of the
-// centre-padded (200 each side, reflect) signal, which is itself the
-// utterance zero-padded / trimmed to n_pad samples (ctc.py:85-90).  Writes the
-// Hann-windowed frames, row-major [b*T + t][400], for the DFT GEMM.
-__global__ __launch_bounds__(256) void ctc_frames_kernel(const float* __restrict__ audio, int64_t stride, int n_valid,
-                                                         int n_pad, int T, int64_t rows, float* __restrict__ frames) {
-  const int64_t total = rows * kNfft;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t r = i / kNfft;
-    const int n = (int)(i - r * kNfft);
-    const int64_t b = r / T;
-    const int t = (int)(r - b * T);
-    int p = t * kHop - kNfft / 2 + n;
-    p = p < 0 ? -p : p;
-    p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
-    const float v = p < n_valid ? audio[b * stride + p] : 0.0f;
-    float sn, cs;
-    sincospif(2.0f * (float)n / (float)kNfft, &sn, &cs);
-    frames[i] = v * (0.5f - 0.5f * cs);   // periodic Hann(400)
-  }
+// ---------------------------------------------------------------------------
+// X1 as one kernel: frames -> 400-point real DFT by FFT -> power -> HTK mel ->
+// ln(+1e-8).  The DFT is 400 = 20 x 20 four-step (n = 20 n1 + n2,
+// k = k1 + 20 k2): stage 1, lane (frame, n2) takes its 20 real samples
+// x[20 n1 + n2] (reflect-padded, Hann-windowed) through an in-register DFT-20
+// over n1 -> A[n2][k1] (k1 = 0..10 kept: real input, A[n2][20-k1] = conj);
+// stage 2, lane (frame, k1), k1 = 0..19, gathers A[.][k1] through LDS (conj of
+// A[.][20-k1] for k1 > 10), twiddles by W400^(n2 k1) (LDS table) and runs a
+// DFT-20 over n2 -> X[k1 + 20 k2].  Each DFT-20 is 4 x DFT-5 + constant
+// twiddles + 5 x DFT-4, packed fp32.  Three frames per wave (60 lanes), one
+// LDS region per wave, no block barrier in the loop.  ~4.6 kflop per frame
+// instead of the 321 kflop of the DFT-as-GEMM it replaces.
+// ---------------------------------------------------------------------------
+constexpr int kFftWaves = 4, kFftFrames = 3;           // frames per wave pass
+constexpr int kAPitch = 11;                             // A[f][n2][k1], k1 = 0..10 (float2)
+constexpr int kPwPitch = 204;
+struct CtcFftLds {
+  float win[kNfft];
+  f2 tw[20][20];                                        // W400^(n2 k1), [k1][n2]
+  f2 a[kFftWaves][kFftFrames * 20 * kAPitch];
+  float pw[kFftWaves][kFftFrames][kPwPitch];
+};
+
+// W20^e = exp(-2 pi i e / 20).
+__constant__ constexpr float kW20c[20] = {1.000000000e+00f, 9.510565163e-01f, 8.090169944e-01f, 5.877852523e-01f, 3.090169944e-01f, 0.000000000e+00f, -3.090169944e-01f, -5.877852523e-01f, -8.090169944e-01f, -9.510565163e-01f, -1.000000000e+00f, -9.510565163e-01f, -8.090169944e-01f, -5.877852523e-01f, -3.090169944e-01f, 0.000000000e+00f, 3.090169944e-01f, 5.877852523e-01f, 8.090169944e-01f, 9.510565163e-01f};
+__constant__ constexpr float kW20s[20] = {0.000000000e+00f, -3.090169944e-01f, -5.877852523e-01f, -8.090169944e-01f, -9.510565163e-01f, -1.000000000e+00f, -9.510565163e-01f, -8.090169944e-01f, -5.877852523e-01f, -3.090169944e-01f, 0.000000000e+00f, 3.090169944e-01f, 5.877852523e-01f, 8.090169944e-01f, 9.510565163e-01f, 1.000000000e+00f, 9.510565163e-01f, 8.090169944e-01f, 5.877852523e-01f, 3.090169944e-01f};
+__device__ __forceinline__ f2 w20(int e) { return f2{kW20c[e % 20], kW20s[e % 20]}; }
+
+// In-register DFT-5 (forward), natural order in and out.
+__device__ __forceinline__ void dft5(f2& x0, f2& x1, f2& x2, f2& x3, f2& x4) {
+  constexpr float c1 = 0.30901699437494742f, c2 = -0.80901699437494742f;
+  constexpr float s1 = 0.95105651629515357f, s2 = 0.58778525229247313f;
+  const f2 t1 = x1 + x4, t2 = x2 + x3, t3 = x1 - x4, t4 = x2 - x3;
+  const f2 a1 = fma2(f2{c2, c2}, t2, fma2(f2{c1, c1}, t1, x0));
+  const f2 a2 = fma2(f2{c1, c1}, t2, fma2(f2{c2, c2}, t1, x0));
+  const f2 b1 = fma2(f2{s2, s2}, t4, f2{s1, s1} * t3);   // Y1 = a1 - i b1, Y4 = a1 + i b1
+  const f2 b2 = fma2(f2{-s1, -s1}, t4, f2{s2, s2} * t3); // Y2 = a2 - i b2, Y3 = a2 + i b2
+  x0 = x0 + t1 + t2;
+  x1 = sub_ib(a1, b1);
+  x4 = add_ib(a1, b1);
+  x2 = sub_ib(a2, b2);
+  x3 = add_ib(a2, b2);
 }
 
-// spec [rows][402] = (Re[0..200], Im[0..200]) -> power -> HTK mel -> ln(+1e-8), one wave per row.
-__global__ __launch_bounds__(256) void ctc_power_mel_kernel(const float* __restrict__ spec, int64_t rows,
-                                                            const int* __restrict__ fb_start,
-                                                            const int* __restrict__ fb_len,
-                                                            const int* __restrict__ fb_off,
-                                                            const float* __restrict__ fb_w, float* __restrict__ feats) {
-  __shared__ float pw[4][kBins + 3];
+// In-register DFT-20 (forward): x[0..19] natural order -> X[k] in x[k].
+// n = 4 m + r: DFT-5 over m per r, twiddle W20^(r ka), DFT-4 over r per ka;
+// X[ka + 5 kb] comes out of the DFT-4 of column ka at position kb.
+__device__ __forceinline__ void dft20(f2 (&x)[20]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dft5(x[r], x[4 + r], x[8 + r], x[12 + r], x[16 + r]);   // B[r][ka] at x[4 ka + r]
+#pragma unroll
+  for (int r = 1; r < 4; ++r)
+#pragma unroll
+    for (int ka = 1; ka < 5; ++ka) x[4 * ka + r] = cmulc(x[4 * ka + r], w20(r * ka));
+  f2 y[20];
+#pragma unroll
+  for (int ka = 0; ka < 5; ++ka) {
+    f2 b0 = x[4 * ka], b1 = x[4 * ka + 1], b2 = x[4 * ka + 2], b3 = x[4 * ka + 3];
+    dft4(b0, b1, b2, b3);
+    y[ka] = b0;
+    y[ka + 5] = b1;
+    y[ka + 10] = b2;
+    y[ka + 15] = b3;
+  }
+#pragma unroll
+  for (int k = 0; k < 20; ++k) x[k] = y[k];
+}
+
+__global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __restrict__ audio, int64_t stride,
+                                                             int n_valid, int n_pad, int T, int64_t rows,
+                                                             const float* __restrict__ win_g,
+                                                             const float* __restrict__ tw_g,
+                                                             const int* __restrict__ fb_start,
+                                                             const int* __restrict__ fb_len,
+                                                             const int* __restrict__ fb_off,
+                                                             const float* __restrict__ fb_w,
+                                                             float* __restrict__ feats) {
+  __shared__ CtcFftLds L;
+  for (int i = threadIdx.x; i < kNfft; i += 256) L.win[i] = win_g[i];
+  for (int i = threadIdx.x; i < 400; i += 256) L.tw[i / 20][i % 20] = f2{tw_g[2 * i], tw_g[2 * i + 1]};
+  __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int64_t r0 = (int64_t)blockIdx.x * 4; r0 < rows; r0 += (int64_t)gridDim.x * 4) {
-    const int64_t r = r0 + wv;
-    if (r < rows) {   // wave-uniform
-      const float* x = spec + r * (2 * kBins);
-      for (int k = lane; k < kBins; k += 64) {
-        const float re = x[k], im = x[kBins + k];
-        pw[wv][k] = __builtin_fmaf(re, re, im * im);
+  const int f = lane / 20, q = lane - 20 * (lane / 20);   // frame slot (3 = idle lanes 60-63), n2 / k1
+  f2* A = L.a[wv];
+  float* PW = &L.pw[wv][0][0];
+  const int64_t passes = (rows + kFftFrames - 1) / kFftFrames;
+  for (int64_t ps = (int64_t)blockIdx.x * kFftWaves + wv; ps < passes; ps += (int64_t)gridDim.x * kFftWaves) {
+    const int64_t row = ps * kFftFrames + f;
+    const bool act = f < kFftFrames && row < rows;
+    // stage 1: lane (f, n2 = q): DFT-20 over n1 of x[20 n1 + n2]
+    if (act) {
+      const int64_t b = row / T;
+      const int t = (int)(row - b * T);
+      const float* xa = audio + b * stride;
+      f2 v[20];
+#pragma unroll
+      for (int n1 = 0; n1 < 20; ++n1) {
+        const int n = 20 * n1 + q;
+        int p = t * kHop - kNfft / 2 + n;
+        p = p < 0 ? -p : p;
+        p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
+        const float s = p < n_valid ? xa[p] : 0.0f;
+        v[n1] = f2{s * L.win[n], 0.0f};
       }
-      wave_lds_sync();
-      for (int m = lane; m < kMels; m += 64) {
-        float acc = 0.0f;
+      dft20(v);
+#pragma unroll
+      for (int k1 = 0; k1 <= 10; ++k1) A[(f * 20 + q) * kAPitch + k1] = v[k1];
+    }
+    wave_lds_sync();
+    // stage 2: lane (f, k1 = q): twiddle + DFT-20 over n2 -> X[k1 + 20 k2]
+    if (act) {
+      const bool mirror = q > 10;
+      const int kc = mirror ? 20 - q : q;
+      const f2 sg = mirror ? f2{1.0f, -1.0f} : f2{1.0f, 1.0f};   // conj for k1 > 10
+      f2 v[20];
+#pragma unroll
+      for (int n2 = 0; n2 < 20; ++n2) v[n2] = cmul2(A[(f * 20 + n2) * kAPitch + kc] * sg, L.tw[q][n2]);
+      dft20(v);
+      float* pw = PW + f * kPwPitch;
+#pragma unroll
+      for (int k2 = 0; k2 < 10; ++k2) pw[q + 20 * k2] = __builtin_fmaf(v[k2].x, v[k2].x, v[k2].y * v[k2].y);
+      if (q == 0) pw[200] = __builtin_fmaf(v[10].x, v[10].x, v[10].y * v[10].y);
+    }
+    wave_lds_sync();
+    // power -> HTK mel (CSR) -> ln(+1e-8): task (frame, mel) over the wave's lanes
+    for (int i = lane; i < kFftFrames * kMels; i += 64) {
+      const int ff = i / kMels, m = i - kMels * (i / kMels);
+      const int64_t r = ps * kFftFrames + ff;
+      if (r < rows) {
         const int s0 = fb_start[m], n = fb_len[m], o = fb_off[m];
-        for (int j = 0; j < n; ++j) acc = __builtin_fmaf(pw[wv][s0 + j], fb_w[o + j], acc);
+        const float* pw = PW + ff * kPwPitch + s0;
+        float acc = 0.0f;
+        for (int j = 0; j < n; ++j) acc = __builtin_fmaf(pw[j], fb_w[o + j], acc);
         feats[r * kMels + m] = logf(acc + 1e-8f);
       }
     }
@@ -517,12 +606,11 @@ struct wk_ctc {
   __half* wih16[2];     // fp16 copies (precision 1)
   __half* whh16_pk[2];  // per layer: [2 dir][24 tiles][8 k-steps][64 lanes][4]
   __half* out_w16;
-  float* dft;           // [402][400]: cos rows k = 0..200, then -sin rows
+  float* fft_win;       // [400] periodic Hann
+  float* fft_tw;        // [20 k1][20 n2] W400^(n2 k1), complex
   int *fb_start, *fb_len, *fb_off;
   float* fb_w;
   // workspaces (grown on demand)
-  size_t fe_rows;
-  float *frames, *spec;
   size_t ws_rows;
   float *x0, *gi, *y0, *y1, *logits;
   __half *x0h, *y0h, *y1h, *logits16;
@@ -547,19 +635,11 @@ void free_ws(wk_ctc* c) {
   c->ws_rows = 0;
 }
 
-void free_fe(wk_ctc* c) {
-  (void)hipFree(c->frames);
-  (void)hipFree(c->spec);
-  c->frames = c->spec = nullptr;
-  c->fe_rows = 0;
-}
-
 void free_all(wk_ctc* c) {
   free_ws(c);
-  free_fe(c);
   void* ps[] = {c->enc_w, c->enc_b, c->ln_g, c->ln_b, c->wih[0], c->wih[1], c->bih[0], c->bih[1], c->bhh[0],
                 c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->fb_w, c->wih16[0], c->wih16[1],
-                c->out_w16, c->dft, c->fb_start, c->fb_len, c->fb_off, c->whh16_pk[0], c->whh16_pk[1]};
+                c->out_w16, c->fft_win, c->fft_tw, c->fb_start, c->fb_len, c->fb_off, c->whh16_pk[0], c->whh16_pk[1]};
   for (void* q : ps) (void)hipFree(q);
   if (c->blas) rocblas_destroy_handle(c->blas);
 }
@@ -663,16 +743,18 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     if (e == hipSuccess) e = upload(&c->out_w, ow, (size_t)V * 2 * H);
     if (e == hipSuccess && c->f16) e = upload_f16(&c->out_w16, ow, (size_t)V * 2 * H);
     if (e == hipSuccess) e = upload(&c->out_b, take(V), V);
-    // DFT matrix of the 400-point frames: rows k = 0..200 cos(2 pi n k / 400), rows 201.. -sin
+    // FFT tables: periodic Hann(400) and the four-step twiddles W400^(n2 k1), in double -> fp32
     {
-      std::vector<float> d((size_t)2 * kBins * kNfft);
-      for (int k = 0; k < kBins; ++k)
-        for (int n = 0; n < kNfft; ++n) {
-          const double ang = 2.0 * M_PI * (double)((n * k) % kNfft) / kNfft;
-          d[(size_t)k * kNfft + n] = (float)cos(ang);
-          d[(size_t)(kBins + k) * kNfft + n] = (float)-sin(ang);
+      std::vector<float> wnd(kNfft), tw(2 * 400);
+      for (int n = 0; n < kNfft; ++n) wnd[n] = (float)(0.5 - 0.5 * cos(2.0 * M_PI * n / kNfft));
+      for (int k1 = 0; k1 < 20; ++k1)
+        for (int n2 = 0; n2 < 20; ++n2) {
+          const double ang = -2.0 * M_PI * (double)(n2 * k1) / kNfft;
+          tw[2 * (k1 * 20 + n2)] = (float)cos(ang);
+          tw[2 * (k1 * 20 + n2) + 1] = (float)sin(ang);
         }
-      if (e == hipSuccess) e = upload(&c->dft, d.data(), d.size());
+      if (e == hipSuccess) e = upload(&c->fft_win, wnd.data(), wnd.size());
+      if (e == hipSuccess) e = upload(&c->fft_tw, tw.data(), tw.size());
     }
     // mel filterbank as CSR (per filter: first bin, count, weights)
     std::vector<float> fb;
@@ -724,24 +806,12 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
   return on_device(c->cfg.device, [&]() -> wk_status {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
-    if ((size_t)rows > c->fe_rows) {
-      if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
-      free_fe(c);
-      if ((e = hipMalloc(&c->frames, sizeof(float) * rows * kNfft)) != hipSuccess ||
-          (e = hipMalloc(&c->spec, sizeof(float) * rows * 2 * kBins)) != hipSuccess) {
-        free_fe(c);
-        return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_ctc_features workspace");
-      }
-      c->fe_rows = rows;
-    }
-    if (rocblas_set_stream(c->blas, st) != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_set_stream");
     const int nv = n_valid < n_samples ? n_valid : n_samples;
-    hipLaunchKernelGGL(ctc_frames_kernel, dim3(16 * c->n_cu), dim3(256), 0, st, d_audio, stride, nv, n_samples, T, rows,
-                       c->frames);
-    wk_status s = gemm_nt(c->blas, rows, 2 * kBins, kNfft, c->frames, c->dft, c->spec, false);   // DFT as a GEMM
-    if (s != WK_OK) return s;
-    hipLaunchKernelGGL(ctc_power_mel_kernel, dim3((unsigned)((rows + 3) / 4 < 16 * c->n_cu ? (rows + 3) / 4 : 16 * c->n_cu)),
-                       dim3(256), 0, st, c->spec, rows, c->fb_start, c->fb_len, c->fb_off, c->fb_w, d_feats);
+    const int64_t passes = (rows + kFftFrames - 1) / kFftFrames;
+    const int64_t blocks = (passes + kFftWaves - 1) / kFftWaves;
+    hipLaunchKernelGGL(ctc_logmel_fft_kernel, dim3((unsigned)(blocks < 8 * c->n_cu ? blocks : 8 * c->n_cu)), dim3(256), 0,
+                       st, d_audio, stride, nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->fb_start, c->fb_len,
+                       c->fb_off, c->fb_w, d_feats);
     hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
     e = hipGetLastError();
     return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_features launch");
