@@ -489,7 +489,7 @@ __global__ __launch_bounds__(256) void ctc_argmax_kernel(const LT* __restrict__ 
     const float lse = mx + logf(s);
     for (int v = lane; v < V; v += 64) log_probs[r * V + v] = (float)x[v] + bias[v] - lse;
   }
-  if (lane == 0) best[r] = arg;
+  if (lane == 0 && best) best[r] = arg;
 }
 
 // Argmax only (no log_softmax requested: the greedy decode needs just the
@@ -565,6 +565,133 @@ __global__ void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T
   }
   for (int t = n; t < T; ++t) o[t] = -1;
   lengths[b] = n;
+}
+
+// ---------------------------------------------------------------------------
+// X2 output layer + X3 argmax, fused (fp16 mode): best[r] = first argmax over
+// v of (y[r] . W[v] + b[v]) with y [rows][256] and W [V][256] in fp16, fp32
+// accumulation on v_mfma_f32_16x16x32_f16 -- the [rows][V] logits never touch
+// HBM (they were 2 x 9.9 GB of traffic per 4096 utterances).  A workgroup owns
+// 256 rows: each of its 8 waves keeps its 32 rows' A fragments in VGPRs
+// (2 row tiles x 8 K-steps) and walks V in 64-column tiles of W staged through
+// a double-buffered LDS image (row pitch 264 halfs: the 16 column lanes of a
+// ds_read_b128 land on distinct banks), one barrier per tile.  Each lane keeps
+// a running (max, index) for its 8 rows over its columns, visited in increasing
+// order, then 16-lane shuffles pick the first maximum (torch.max semantics).
+// LOGITS = true also stores fp16 logits for the log_softmax kernel; the argmax
+// is this kernel's in both cases, so tokens do not depend on log-probs being
+// requested.
+// ---------------------------------------------------------------------------
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+constexpr int kOutK = 2 * kH, kOutBN = 64, kOutPitch = kOutK + 8, kOutWaves = 8, kOutRows = 32 * kOutWaves;
+
+template <bool LOGITS>
+__global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const __half* __restrict__ y,
+                                                                          const __half* __restrict__ w,
+                                                                          const float* __restrict__ bias, int64_t rows,
+                                                                          int V, __half* __restrict__ logits,
+                                                                          int* __restrict__ best) {
+  __shared__ __attribute__((aligned(16))) _Float16 bt[2][kOutBN * kOutPitch];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * kOutRows + 32 * wv;
+  // A fragments: rows row0 + 16 rf + li, k = 32 s + 8 lg .. +7
+  h8 a[2][8];
+#pragma unroll
+  for (int rf = 0; rf < 2; ++rf) {
+    const int64_t r = row0 + 16 * rf + li;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (r < rows) v = *reinterpret_cast<const uint4*>(y + r * kOutK + 32 * st + 8 * lg);
+      a[rf][st] = __builtin_bit_cast(h8, v);
+    }
+  }
+  const int NT = (V + kOutBN - 1) / kOutBN;
+  // W tile nt -> registers: 64 rows x 32 16-byte chunks, 4 per thread
+  uint4 pre[4];
+  auto fetch = [&](int nt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
+      const int v = nt * kOutBN + rr;
+      pre[i] = v < V ? *reinterpret_cast<const uint4*>(w + (int64_t)v * kOutK + 8 * ch) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
+      *reinterpret_cast<uint4*>(&bt[buf][rr * kOutPitch + 8 * ch]) = pre[i];
+    }
+  };
+  fetch(0);
+  stash(0);
+  __syncthreads();
+  float mx[2][4];
+  int ix[2][4];
+#pragma unroll
+  for (int rf = 0; rf < 2; ++rf)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { mx[rf][i] = -INFINITY; ix[rf][i] = 0; }
+  for (int nt = 0; nt < NT; ++nt) {
+    if (nt + 1 < NT) fetch(nt + 1);
+    const _Float16* b = bt[nt & 1];
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int rf = 0; rf < 2; ++rf)
+#pragma unroll
+      for (int cf = 0; cf < 4; ++cf) acc[rf][cf] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      h8 bf[4];
+#pragma unroll
+      for (int cf = 0; cf < 4; ++cf)
+        bf[cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 32 * st + 8 * lg);
+#pragma unroll
+      for (int rf = 0; rf < 2; ++rf)
+#pragma unroll
+        for (int cf = 0; cf < 4; ++cf)
+          acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf[cf], acc[rf][cf], 0, 0, 0);
+    }
+    // epilogue: column v = 64 nt + 16 cf + li, rows row0 + 16 rf + 4 lg + i
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf) {
+      const int v = nt * kOutBN + 16 * cf + li;
+      if (v < V) {
+        const float bb = bias[v];
+#pragma unroll
+        for (int rf = 0; rf < 2; ++rf)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float z = acc[rf][cf][i] + bb;
+            if (z > mx[rf][i]) { mx[rf][i] = z; ix[rf][i] = v; }
+            if (LOGITS) {
+              const int64_t r = row0 + 16 * rf + 4 * lg + i;
+              if (r < rows) logits[r * V + v] = __float2half(acc[rf][cf][i]);
+            }
+          }
+      }
+    }
+    if (nt + 1 < NT) stash((nt + 1) & 1);
+    __syncthreads();
+  }
+  // first maximum across the 16 column lanes of each row
+#pragma unroll
+  for (int rf = 0; rf < 2; ++rf)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float m = mx[rf][i];
+      int k = ix[rf][i];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float om = __shfl_xor(m, o, 64);
+        const int ok = __shfl_xor(k, o, 64);
+        if (om > m || (om == m && ok < k)) { m = om; k = ok; }
+      }
+      const int64_t r = row0 + 16 * rf + 4 * lg + i;
+      if (li == 0 && r < rows) best[r] = k;
+    }
 }
 
 // HTK mel filterbank of torchaudio.functional.melscale_fbanks(201, 0, 8000, 80, 16000), in fp32 like torch.
@@ -873,21 +1000,30 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
       in16 = ys16[l];
     }
     if (f16) hipLaunchKernelGGL(to_f16_kernel, dim3(big_grid), dim3(256), 0, st, c->y1, c->y1h, rows * 2 * H);
-    wk_status s = f16 ? gemm_nt(c->blas, rows, V, 2 * H, c->y1h, c->out_w16, c->logits16, true, true)
-                      : gemm_nt(c->blas, rows, V, 2 * H, c->y1, c->out_w, c->logits, false);
+    if (f16) {
+      // fused output layer + argmax; fp16 logits are written only for log_softmax
+      const dim3 og((unsigned)((rows + kOutRows - 1) / kOutRows));
+      if (d_log_probs) {
+        hipLaunchKernelGGL(ctc_out_argmax16_kernel<true>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
+                           c->out_b, rows, V, c->logits16, c->best);
+        hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits16,
+                           c->out_b, rows, V, d_log_probs, (int*)nullptr);
+      } else {
+        hipLaunchKernelGGL(ctc_out_argmax16_kernel<false>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
+                           c->out_b, rows, V, (__half*)nullptr, c->best);
+      }
+      hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st, c->best, batch, T,
+                         d_tokens, d_lengths);
+      e = hipGetLastError();
+      return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_forward launch");
+    }
+    wk_status s = gemm_nt(c->blas, rows, V, 2 * H, c->y1, c->out_w, c->logits, false);
     if (s != WK_OK) return s;
-    const int nv = f16 ? Vec<__half>::N : Vec<float>::N;
-    const bool arg_only = !d_log_probs && V % nv == 0 && V / nv <= 64 * kArgChunks && V <= 16384;
+    const bool arg_only = !d_log_probs && V % Vec<float>::N == 0 && V / Vec<float>::N <= 64 * kArgChunks && V <= 16384;
     const unsigned ag = (unsigned)((rows + 3) / 4 < 8 * c->n_cu ? (rows + 3) / 4 : 8 * c->n_cu);
-    if (arg_only && f16)
-      hipLaunchKernelGGL(ctc_argmax_only_kernel<__half>, dim3(ag), dim3(256), V * sizeof(float), st, c->logits16,
-                         c->out_b, rows, V, c->best);
-    else if (arg_only)
+    if (arg_only)
       hipLaunchKernelGGL(ctc_argmax_only_kernel<float>, dim3(ag), dim3(256), V * sizeof(float), st, c->logits,
                          c->out_b, rows, V, c->best);
-    else if (f16)   // fp16 logits: half the HBM traffic of the [rows][V] intermediate
-      hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits16,
-                         c->out_b, rows, V, d_log_probs, c->best);
     else
       hipLaunchKernelGGL(ctc_argmax_kernel<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits,
                          c->out_b, rows, V, d_log_probs, c->best);
