@@ -224,10 +224,15 @@ __global__ __launch_bounds__(1024) void ctc_zscore_kernel(float* __restrict__ fe
 // ---------------------------------------------------------------------------
 // X2a: encoder Linear(80,128) + LayerNorm(128) + ReLU, one wave per row
 // ---------------------------------------------------------------------------
+// OT = float, or __half in fp16 mode (the next GEMM's operand, written directly).
+__device__ __forceinline__ void st_out(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st_out(__half* p, float v) { *p = __float2half(v); }
+
+template <typename OT>
 __global__ __launch_bounds__(256) void ctc_encoder_kernel(const float* __restrict__ in, int64_t rows,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
                                                           const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float* __restrict__ out) {
+                                                          const float* __restrict__ beta, OT* __restrict__ out) {
   __shared__ float wt[kMels][kH];   // transposed: wt[k][o]
   __shared__ float xr[4][kMels];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -256,8 +261,8 @@ __global__ __launch_bounds__(256) void ctc_encoder_kernel(const float* __restric
     const float var = wave_sum(d0 * d0 + d1 * d1) * (1.0f / kH);   // biased, as nn.LayerNorm
     const float rs = 1.0f / sqrtf(var + 1e-5f);
     if (act) {
-      out[r * kH + lane] = fmaxf(__builtin_fmaf(d0 * rs, g0, e0), 0.0f);
-      out[r * kH + lane + 64] = fmaxf(__builtin_fmaf(d1 * rs, g1, e1), 0.0f);
+      st_out(out + r * kH + lane, fmaxf(__builtin_fmaf(d0 * rs, g0, e0), 0.0f));
+      st_out(out + r * kH + lane + 64, fmaxf(__builtin_fmaf(d1 * rs, g1, e1), 0.0f));
     }
     wave_lds_sync();
   }
@@ -350,7 +355,7 @@ constexpr int kH16P = kH + 4;   // LDS pitch (halves) of the fp16 state image [b
 __global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const float* __restrict__ gi, const h4* __restrict__ whh_pk,
                                                                 const float* __restrict__ bih,
                                                                 const float* __restrict__ bhh, int64_t B, int T,
-                                                                float* __restrict__ out) {
+                                                                __half* __restrict__ out) {   // fp16: the next GEMM's operand
   __shared__ float hs[2][kH * kHP];
   __shared__ float gh[3 * kH * kHP];
   __shared__ __attribute__((aligned(16))) _Float16 h16[2][kGruBatch * kH16P];
@@ -403,7 +408,7 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const float* __r
         const float c = tanhf(g[2 * kH + u] + bi[2 * kH + u] + r * (gh[(2 * kH + u) * kHP + n] + bh[2 * kH + u]));
         const float hp = hs[cur][u * kHP + n];
         hn = __builtin_fmaf(z, hp - c, c);
-        out[((size_t)b * T + t) * (2 * kH) + dir * kH + u] = hn;
+        out[((size_t)b * T + t) * (2 * kH) + dir * kH + u] = __float2half(hn);
       }
       hs[cur ^ 1][u * kHP + n] = hn;
       h16[cur ^ 1][n * kH16P + u] = (_Float16)hn;
@@ -797,10 +802,6 @@ wk_status gemm_nt(rocblas_handle h, int64_t M, int64_t N, int64_t K, const void*
   return s == rocblas_status_success ? WK_OK : fail(WK_ERR_HIP, "rocblas_gemm_ex failed");
 }
 
-__global__ void to_f16_kernel(const float* __restrict__ in, __half* __restrict__ out, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    out[i] = __float2half(in[i]);
-}
 
 }  // namespace
 
@@ -959,10 +960,10 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
     if ((size_t)rows > c->ws_rows) {   // workspace grows on first use of a larger batch (then reused)
       if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
       free_ws(c);
-      if ((e = hipMalloc(&c->x0, sizeof(float) * rows * H)) != hipSuccess ||
+      if ((!f16 && (e = hipMalloc(&c->x0, sizeof(float) * rows * H)) != hipSuccess) ||
           (e = hipMalloc(&c->gi, sizeof(float) * rows * 6 * H)) != hipSuccess ||
-          (e = hipMalloc(&c->y0, sizeof(float) * rows * 2 * H)) != hipSuccess ||
-          (e = hipMalloc(&c->y1, sizeof(float) * rows * 2 * H)) != hipSuccess ||
+          (!f16 && (e = hipMalloc(&c->y0, sizeof(float) * rows * 2 * H)) != hipSuccess) ||
+          (!f16 && (e = hipMalloc(&c->y1, sizeof(float) * rows * 2 * H)) != hipSuccess) ||
           (!f16 && (e = hipMalloc(&c->logits, sizeof(float) * rows * V)) != hipSuccess) ||
           (e = hipMalloc(&c->best, sizeof(int) * rows)) != hipSuccess ||
           (f16 && (e = hipMalloc(&c->x0h, sizeof(__half) * rows * H)) != hipSuccess) ||
@@ -975,31 +976,32 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
       c->ws_rows = rows;
     }
     if (rocblas_set_stream(c->blas, st) != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_set_stream");
-    const int big_grid = 16 * c->n_cu;
     const int enc_grid = (int)((rows + 3) / 4 < 8 * c->n_cu ? (rows + 3) / 4 : 8 * c->n_cu);
-    hipLaunchKernelGGL(ctc_encoder_kernel, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w, c->enc_b,
-                       c->ln_g, c->ln_b, c->x0);
+    if (f16)
+      hipLaunchKernelGGL(ctc_encoder_kernel<__half>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
+                         c->enc_b, c->ln_g, c->ln_b, c->x0h);
+    else
+      hipLaunchKernelGGL(ctc_encoder_kernel<float>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
+                         c->enc_b, c->ln_g, c->ln_b, c->x0);
     const float* in = c->x0;
     const __half* in16 = c->x0h;
     float* ys[2] = {c->y0, c->y1};
     __half* ys16[2] = {c->y0h, c->y1h};
     for (int l = 0; l < 2; ++l) {
       const int din = l == 0 ? H : 2 * H;
-      if (f16) hipLaunchKernelGGL(to_f16_kernel, dim3(big_grid), dim3(256), 0, st, in, (__half*)in16, rows * din);
       wk_status s = f16 ? gemm_nt(c->blas, rows, 6 * H, din, in16, c->wih16[l], c->gi, true)
                         : gemm_nt(c->blas, rows, 6 * H, din, in, c->wih[l], c->gi, false);
       if (s != WK_OK) return s;
       const dim3 gg((unsigned)((batch + kGruBatch - 1) / kGruBatch), 2);
       if (f16)
         hipLaunchKernelGGL(ctc_gru16_kernel, gg, dim3(kGruThreads), 0, st, c->gi, (const h4*)c->whh16_pk[l], c->bih[l],
-                           c->bhh[l], batch, T, ys[l]);
+                           c->bhh[l], batch, T, ys16[l]);
       else
         hipLaunchKernelGGL(ctc_gru_kernel, gg, dim3(kGruThreads), 0, st, c->gi, c->whh_pk[l], c->bih[l], c->bhh[l],
                            batch, T, ys[l]);
       in = ys[l];
       in16 = ys16[l];
     }
-    if (f16) hipLaunchKernelGGL(to_f16_kernel, dim3(big_grid), dim3(256), 0, st, c->y1, c->y1h, rows * 2 * H);
     if (f16) {
       // fused output layer + argmax; fp16 logits are written only for log_softmax
       const dim3 og((unsigned)((rows + kOutRows - 1) / kOutRows));
