@@ -577,8 +577,8 @@ __global__ void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T
 // v of (y[r] . W[v] + b[v]) with y [rows][256] and W [V][256] in fp16, fp32
 // accumulation on v_mfma_f32_16x16x32_f16 -- the [rows][V] logits never touch
 // HBM (they were 2 x 9.9 GB of traffic per 4096 utterances).  A workgroup owns
-// 256 rows: each of its 8 waves keeps its 32 rows' A fragments in VGPRs
-// (2 row tiles x 8 K-steps) and walks V in 64-column tiles of W staged through
+// kOutRows rows: each of its kOutWaves waves keeps its 16 kOutRF rows' A
+// fragments in VGPRs (kOutRF row tiles x 8 K-steps) and walks V in 64-column tiles of W staged through
 // a double-buffered LDS image (row pitch 264 halfs: the 16 column lanes of a
 // ds_read_b128 land on distinct banks), one barrier per tile.  Each lane keeps
 // a running (max, index) for its 8 rows over its columns, visited in increasing
@@ -588,7 +588,15 @@ __global__ void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T
 // requested.
 // ---------------------------------------------------------------------------
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-constexpr int kOutK = 2 * kH, kOutBN = 64, kOutPitch = kOutK + 8, kOutWaves = 8, kOutRows = 32 * kOutWaves;
+#ifndef WK_OUT_RF
+#define WK_OUT_RF 2      // 16-row MFMA tiles per wave
+#endif
+#ifndef WK_OUT_WAVES
+#define WK_OUT_WAVES 8
+#endif
+constexpr int kOutK = 2 * kH, kOutBN = 64, kOutPitch = kOutK + 8, kOutRF = WK_OUT_RF, kOutWaves = WK_OUT_WAVES;
+constexpr int kOutRows = 16 * kOutRF * kOutWaves, kOutPre = kOutBN * (kOutK / 8) / (64 * kOutWaves);
+static_assert(kOutPre * 64 * kOutWaves == kOutBN * (kOutK / 8), "W tile chunks divide over the threads");
 
 template <bool LOGITS>
 __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const __half* __restrict__ y,
@@ -599,11 +607,11 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   __shared__ __attribute__((aligned(16))) _Float16 bt[2][kOutBN * kOutPitch];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
-  const int64_t row0 = (int64_t)blockIdx.x * kOutRows + 32 * wv;
+  const int64_t row0 = (int64_t)blockIdx.x * kOutRows + 16 * kOutRF * wv;
   // A fragments: rows row0 + 16 rf + li, k = 32 s + 8 lg .. +7
-  h8 a[2][8];
+  h8 a[kOutRF][8];
 #pragma unroll
-  for (int rf = 0; rf < 2; ++rf) {
+  for (int rf = 0; rf < kOutRF; ++rf) {
     const int64_t r = row0 + 16 * rf + li;
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
@@ -614,10 +622,10 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   }
   const int NT = (V + kOutBN - 1) / kOutBN;
   // W tile nt -> registers: 64 rows x 32 16-byte chunks, 4 per thread
-  uint4 pre[4];
+  uint4 pre[kOutPre];
   auto fetch = [&](int nt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kOutPre; ++i) {
       const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
       const int v = nt * kOutBN + rr;
       pre[i] = v < V ? *reinterpret_cast<const uint4*>(w + (int64_t)v * kOutK + 8 * ch) : make_uint4(0, 0, 0, 0);
@@ -625,7 +633,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   };
   auto stash = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kOutPre; ++i) {
       const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
       *reinterpret_cast<uint4*>(&bt[buf][rr * kOutPitch + 8 * ch]) = pre[i];
     }
@@ -633,18 +641,18 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   fetch(0);
   stash(0);
   __syncthreads();
-  float mx[2][4];
-  int ix[2][4];
+  float mx[kOutRF][4];
+  int ix[kOutRF][4];
 #pragma unroll
-  for (int rf = 0; rf < 2; ++rf)
+  for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
     for (int i = 0; i < 4; ++i) { mx[rf][i] = -INFINITY; ix[rf][i] = 0; }
   for (int nt = 0; nt < NT; ++nt) {
     if (nt + 1 < NT) fetch(nt + 1);
     const _Float16* b = bt[nt & 1];
-    f32x4 acc[2][4];
+    f32x4 acc[kOutRF][4];
 #pragma unroll
-    for (int rf = 0; rf < 2; ++rf)
+    for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
       for (int cf = 0; cf < 4; ++cf) acc[rf][cf] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -654,7 +662,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       for (int cf = 0; cf < 4; ++cf)
         bf[cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 32 * st + 8 * lg);
 #pragma unroll
-      for (int rf = 0; rf < 2; ++rf)
+      for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
         for (int cf = 0; cf < 4; ++cf)
           acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf[cf], acc[rf][cf], 0, 0, 0);
@@ -666,7 +674,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       if (v < V) {
         const float bb = bias[v];
 #pragma unroll
-        for (int rf = 0; rf < 2; ++rf)
+        for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float z = acc[rf][cf][i] + bb;
@@ -683,7 +691,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   }
   // first maximum across the 16 column lanes of each row
 #pragma unroll
-  for (int rf = 0; rf < 2; ++rf)
+  for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float m = mx[rf][i];
