@@ -390,7 +390,7 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru_kernel(const float* __res
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 constexpr int kH16P = kH + 4;   // LDS pitch (halves) of the fp16 state image [batch][unit]
 
-__global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const float* __restrict__ gi, const h4* __restrict__ whh_pk,
+__global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const __half* __restrict__ gi, const h4* __restrict__ whh_pk,
                                                                 const float* __restrict__ bih,
                                                                 const float* __restrict__ bhh, int64_t B, int T,
                                                                 __half* __restrict__ out) {   // fp16: the next GEMM's operand
@@ -440,10 +440,11 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const float* __r
       const int64_t b = b0 + n;
       float hn = 0.0f;
       if (b < B) {
-        const float* g = gi + ((size_t)b * T + t) * (6 * kH) + dir * 3 * kH;
-        const float r = sigm(g[u] + bi[u] + gh[u * kHP + n] + bh[u]);
-        const float z = sigm(g[kH + u] + bi[kH + u] + gh[(kH + u) * kHP + n] + bh[kH + u]);
-        const float c = tanhf(g[2 * kH + u] + bi[2 * kH + u] + r * (gh[(2 * kH + u) * kHP + n] + bh[2 * kH + u]));
+        const __half* g = gi + ((size_t)b * T + t) * (6 * kH) + dir * 3 * kH;   // fp16 gates (half the HBM bytes)
+        const float r = sigm(__half2float(g[u]) + bi[u] + gh[u * kHP + n] + bh[u]);
+        const float z = sigm(__half2float(g[kH + u]) + bi[kH + u] + gh[(kH + u) * kHP + n] + bh[kH + u]);
+        const float c = tanhf(__half2float(g[2 * kH + u]) + bi[2 * kH + u] +
+                              r * (gh[(2 * kH + u) * kHP + n] + bh[2 * kH + u]));
         const float hp = hs[cur][u * kHP + n];
         hn = __builtin_fmaf(z, hp - c, c);
         out[((size_t)b * T + t) * (2 * kH) + dir * kH + u] = __float2half(hn);
@@ -1035,12 +1036,12 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
     __half* ys16[2] = {c->y0h, c->y1h};
     for (int l = 0; l < 2; ++l) {
       const int din = l == 0 ? H : 2 * H;
-      wk_status s = f16 ? gemm_nt(c->blas, rows, 6 * H, din, in16, c->wih16[l], c->gi, true)
+      wk_status s = f16 ? gemm_nt(c->blas, rows, 6 * H, din, in16, c->wih16[l], c->gi, true, true)   // fp16 gates
                         : gemm_nt(c->blas, rows, 6 * H, din, in, c->wih[l], c->gi, false);
       if (s != WK_OK) return s;
       const dim3 gg((unsigned)((batch + kGruBatch - 1) / kGruBatch), 2);
       if (f16)
-        hipLaunchKernelGGL(ctc_gru16_kernel, gg, dim3(kGruThreads), 0, st, c->gi, (const h4*)c->whh16_pk[l], c->bih[l],
+        hipLaunchKernelGGL(ctc_gru16_kernel, gg, dim3(kGruThreads), 0, st, (const __half*)c->gi, (const h4*)c->whh16_pk[l], c->bih[l],
                            c->bhh[l], batch, T, ys16[l]);
       else
         hipLaunchKernelGGL(ctc_gru_kernel, gg, dim3(kGruThreads), 0, st, c->gi, c->whh_pk[l], c->bih[l], c->bhh[l],
