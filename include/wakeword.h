@@ -164,9 +164,10 @@ typedef struct {
   int32_t layers;   /* 2 */
   int32_t n_mels;   /* 80 */
   int32_t device;
-  int32_t precision; /* 0: fp32 throughout; 1: GEMM operands fp16 with fp32
-                        accumulation (config 5 "fp16"), recurrence and
-                        front-end stay fp32 */
+  int32_t precision; /* 0: fp32 throughout; 1 (config 5 "fp16"): GEMM and
+                        MFMA operands, activations between layers and the gate
+                        pre-activations in fp16, fp32 accumulation; the gate
+                        arithmetic, state update and front-end stay fp32 */
 } wk_ctc_config;
 typedef struct wk_ctc wk_ctc;
 
