@@ -315,7 +315,12 @@ __global__ __launch_bounds__(256) void ctc_encoder_kernel(const float* __restric
 constexpr int kGruBatch = 16, kGruWaves = 12, kGruThreads = 64 * kGruWaves;
 constexpr int kHP = 17;   // LDS pitch of [unit][batch] images (conflict-free for consecutive units)
 
-__device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + __expf(-v)); }
+// Gate activations on the transcendental unit: v_exp_f32 + v_rcp_f32 (~1 ulp
+// each) instead of an IEEE division and libm tanhf -- the gate math, not the
+// MFMAs, bounded a recurrence step.  tanh(x) = 1 - 2 / (e^2x + 1): exact limits
+// at +-inf, absolute error ~1e-7 near 0.
+__device__ __forceinline__ float sigm(float v) { return __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
+__device__ __forceinline__ float tanh_fast(float v) { return __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(__expf(2.0f * v) + 1.0f), 1.0f); }
 
 __global__ __launch_bounds__(kGruThreads) void ctc_gru_kernel(const float* __restrict__ gi, const float* __restrict__ whh_pk,
                                                               const float* __restrict__ bih, const float* __restrict__ bhh,
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru_kernel(const float* __res
         const float* g = gi + ((size_t)b * T + t) * (6 * kH) + dir * 3 * kH;
         const float r = sigm(g[u] + bi[u] + gh[u * kHP + n] + bh[u]);
         const float z = sigm(g[kH + u] + bi[kH + u] + gh[(kH + u) * kHP + n] + bh[kH + u]);
-        const float c = tanhf(g[2 * kH + u] + bi[2 * kH + u] + r * (gh[(2 * kH + u) * kHP + n] + bh[2 * kH + u]));
+        const float c = tanh_fast(g[2 * kH + u] + bi[2 * kH + u] + r * (gh[(2 * kH + u) * kHP + n] + bh[2 * kH + u]));
         const float hp = hs[cur][u * kHP + n];
         hn = __builtin_fmaf(z, hp - c, c);   // (1 - z) c + z h
         out[((size_t)b * T + t) * (2 * kH) + dir * kH + u] = hn;
@@ -413,8 +418,30 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const __half* __
   for (int i = tid; i < kH * kHP; i += kGruThreads) hs[0][i] = 0.0f;
   for (int i = tid; i < kGruBatch * kH16P; i += kGruThreads) h16[0][i] = (_Float16)0.0f;
   __syncthreads();
+  // Each thread owns one unit u and the batch slots n = nb + 6 j (768 = 6 x 128):
+  // its biases live in registers, and its fp16 gate inputs for step + 1 are
+  // loaded while step's MFMAs run (they do not depend on the recurrence).
+  const int u = tid & (kH - 1), nb = tid >> 7;
+  constexpr int kSlots = (kGruBatch + 5) / 6;
   const float* bi = bih + dir * 3 * kH;
   const float* bh = bhh + dir * 3 * kH;
+  const float b_r = bi[u] + bh[u], b_z = bi[kH + u] + bh[kH + u], bi_c = bi[2 * kH + u], bh_c = bh[2 * kH + u];
+  __half g_r[kSlots], g_z[kSlots], g_c[kSlots];
+  auto load_gates = [&](int step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) {
+      const int n = nb + 6 * j;
+      const int64_t b = b0 + n;
+      if (n < kGruBatch && b < B && step < T) {
+        const __half* g = gi + ((size_t)b * T + t) * (6 * kH) + dir * 3 * kH;
+        g_r[j] = g[u];
+        g_z[j] = g[kH + u];
+        g_c[j] = g[2 * kH + u];
+      }
+    }
+  };
+  load_gates(0);
   int cur = 0;
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? step : T - 1 - step;
@@ -435,16 +462,16 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const __half* __
       }
     }
     __syncthreads();
-    for (int e = tid; e < kGruBatch * kH; e += kGruThreads) {
-      const int n = e >> 7, u = e & (kH - 1);
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) {
+      const int n = nb + 6 * j;
+      if (n >= kGruBatch) continue;
       const int64_t b = b0 + n;
       float hn = 0.0f;
       if (b < B) {
-        const __half* g = gi + ((size_t)b * T + t) * (6 * kH) + dir * 3 * kH;   // fp16 gates (half the HBM bytes)
-        const float r = sigm(__half2float(g[u]) + bi[u] + gh[u * kHP + n] + bh[u]);
-        const float z = sigm(__half2float(g[kH + u]) + bi[kH + u] + gh[(kH + u) * kHP + n] + bh[kH + u]);
-        const float c = tanhf(__half2float(g[2 * kH + u]) + bi[2 * kH + u] +
-                              r * (gh[(2 * kH + u) * kHP + n] + bh[2 * kH + u]));
+        const float r = sigm(__half2float(g_r[j]) + gh[u * kHP + n] + b_r);
+        const float z = sigm(__half2float(g_z[j]) + gh[(kH + u) * kHP + n] + b_z);
+        const float c = tanh_fast(__half2float(g_c[j]) + bi_c + r * (gh[(2 * kH + u) * kHP + n] + bh_c));
         const float hp = hs[cur][u * kHP + n];
         hn = __builtin_fmaf(z, hp - c, c);
         out[((size_t)b * T + t) * (2 * kH) + dir * kH + u] = __float2half(hn);
@@ -452,6 +479,7 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const __half* __
       hs[cur ^ 1][u * kHP + n] = hn;
       h16[cur ^ 1][n * kH16P + u] = (_Float16)hn;
     }
+    load_gates(step + 1);
     cur ^= 1;
     __syncthreads();
   }
