@@ -64,7 +64,10 @@ constexpr int kNfft = 400, kHop = 160, kBins = kNfft / 2 + 1, kMels = 80, kH = 1
 constexpr int kFftWaves = 4, kFftFrames = 3;           // frames per wave pass
 constexpr int kAPitch = 11;                             // A[f][n2][k1], k1 = 0..10 (float2)
 constexpr int kPwPitch = 204;
+constexpr int kFbMaxW = 640;                           // CSR mel weights kept in LDS (host checks nnz)
 struct CtcFftLds {
+  float fbw[kFbMaxW];
+  int fbs[kMels], fbl[kMels], fbo[kMels];
   float win[kNfft];
   f2 tw[20][20];                                        // W400^(n2 k1), [k1][n2]
   f2 a[kFftWaves][kFftFrames * 20 * kAPitch];
@@ -123,11 +126,17 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
                                                              const int* __restrict__ fb_start,
                                                              const int* __restrict__ fb_len,
                                                              const int* __restrict__ fb_off,
-                                                             const float* __restrict__ fb_w,
+                                                             const float* __restrict__ fb_w, int n_fbw,
                                                              float* __restrict__ feats) {
   __shared__ CtcFftLds L;
   for (int i = threadIdx.x; i < kNfft; i += 256) L.win[i] = win_g[i];
   for (int i = threadIdx.x; i < 400; i += 256) L.tw[i / 20][i % 20] = f2{tw_g[2 * i], tw_g[2 * i + 1]};
+  for (int i = threadIdx.x; i < kMels; i += 256) {
+    L.fbs[i] = fb_start[i];
+    L.fbl[i] = fb_len[i];
+    L.fbo[i] = fb_off[i];
+  }
+  for (int i = threadIdx.x; i < n_fbw; i += 256) L.fbw[i] = fb_w[i];
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int f = lane / 20, q = lane - 20 * (lane / 20);   // frame slot (3 = idle lanes 60-63), n2 / k1
@@ -177,11 +186,11 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
       const int ff = i / kMels, m = i - kMels * (i / kMels);
       const int64_t r = ps * kFftFrames + ff;
       if (r < rows) {
-        const int s0 = fb_start[m], n = fb_len[m], o = fb_off[m];
+        const int s0 = L.fbs[m], n = L.fbl[m], o = L.fbo[m];
         const float* pw = PW + ff * kPwPitch + s0;
         float acc = 0.0f;
-        for (int j = 0; j < n; ++j) acc = __builtin_fmaf(pw[j], fb_w[o + j], acc);
-        feats[r * kMels + m] = logf(acc + 1e-8f);
+        for (int j = 0; j < n; ++j) acc = __builtin_fmaf(pw[j], L.fbw[o + j], acc);
+        feats[r * kMels + m] = wk_logf(acc + 1e-8f);
       }
     }
     wave_lds_sync();
@@ -817,6 +826,7 @@ struct wk_ctc {
   float* fft_tw;        // [20 k1][20 n2] W400^(n2 k1), complex
   int *fb_start, *fb_len, *fb_off;
   float* fb_w;
+  int n_fbw;            // CSR weight count (<= kFbMaxW)
   // workspaces (grown on demand)
   size_t ws_rows;
   float *x0, *gi, *y0, *y1, *logits;
@@ -978,6 +988,8 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     if (e == hipSuccess) e = upload(&c->fb_len, ln.data(), kMels);
     if (e == hipSuccess) e = upload(&c->fb_off, off.data(), kMels);
     if (e == hipSuccess) e = upload(&c->fb_w, wv.data(), wv.size());
+    c->n_fbw = (int)wv.size();
+    if (e == hipSuccess && c->n_fbw > kFbMaxW) e = hipErrorInvalidValue;   // LDS copy in ctc_logmel_fft_kernel
     if (e != hipSuccess) {
       free_all(c);
       free(c);
@@ -1014,7 +1026,7 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
     const int64_t blocks = (passes + kFftWaves - 1) / kFftWaves;
     hipLaunchKernelGGL(ctc_logmel_fft_kernel, dim3((unsigned)(blocks < 8 * c->n_cu ? blocks : 8 * c->n_cu)), dim3(256), 0,
                        st, d_audio, stride, nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->fb_start, c->fb_len,
-                       c->fb_off, c->fb_w, d_feats);
+                       c->fb_off, c->fb_w, c->n_fbw, d_feats);
     hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
     e = hipGetLastError();
     return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_features launch");
