@@ -116,3 +116,27 @@ def test_ctc_fp16_gemm_mode(ctc):
     top2 = torch.topk(ref_lp, 2, dim=-1).values
     ok = (top2[..., 0] - top2[..., 1]) > 0.2
     assert (lp.argmax(-1) == ref_lp.argmax(-1))[ok].all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("vocab", [37, 100, 4000])
+def test_ctc_fp16_ragged_vocab(vocab):
+    """The fused fp16 output layer + argmax walks V in 64-column tiles: a
+    vocabulary that is not a multiple of 64 (and a large one) must give the
+    oracle's decisions on confident frames, with and without log-probs."""
+    import wakeword
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    m = CO.make_model(vocab, seed=11)
+    g16 = wakeword.CTCModel(CO.flat_weights(m), vocab, precision="fp16")
+    feats = CO.features(torch.from_numpy(O.synth_clips(13, 0, 3, 48000)))
+    with torch.no_grad():
+        ref_lp = m(feats)
+    seqs_lp, lp = g16.forward(feats, return_log_probs=True)
+    seqs = g16.forward(feats)
+    assert seqs == seqs_lp
+    lp = lp.cpu()
+    assert lp.shape[-1] == vocab and np.abs((lp - ref_lp).numpy()).max() <= 0.05
+    top2 = torch.topk(ref_lp, 2, dim=-1).values
+    ok = (top2[..., 0] - top2[..., 1]) > 0.2
+    assert (lp.argmax(-1) == ref_lp.argmax(-1))[ok].all()
