@@ -5,6 +5,7 @@
 #include <math.h>
 
 #include <mutex>
+#include <new>
 #include <vector>
 #include <string>
 
@@ -14,6 +15,14 @@
 struct wk_handle {
   wk_config cfg;
   int n_cu;
+  unsigned* h_err;       // protocol error word of the fused kernel: pinned, mapped host memory ...
+  unsigned* d_err;       // ... and its device alias (the kernel writes it, the host reads it after a sync)
+  // The unfused / int8 path stages features in d_feats_ws.  Calls may come on
+  // different streams (and host threads), so each use of the workspace waits
+  // on the event recorded after the previous one (stream order across streams).
+  std::mutex ws_mu;
+  hipEvent_t ws_free;
+  bool ws_used;
   float* d_weights;      // packed WK_NUM_WEIGHTS floats, or nullptr (front-end only handle)
   float* d_packed;       // fragment-major weights (wk::pack_fragments) for the fused kernel
   float* d_feats_ws;     // feature workspace for the unfused path
@@ -21,7 +30,8 @@ struct wk_handle {
   uint16_t* d_bf16;      // bf16 conv fragments (WK_PREC_BF16; BF16X3: hi then lo, wk::pack_fragments_bf16)
   int64_t ws_clips;
   int unfused;           // WAKEWORD_UNFUSED=1: front-end + CNN as two kernels (A/B testing)
-  int fused_exp;         // WAKEWORD_FUSED_EXP: role-isolation timing experiments (wrong logits)
+  int fused_exp;         // WAKEWORD_FUSED_EXP, -DWK_DEBUG_EXPERIMENTS builds only: role-isolation timing
+                         // experiments (wrong logits); always 0 in the shipped library
 };
 
 namespace wk {
@@ -67,6 +77,7 @@ const char* wk_status_string(wk_status s) {
     case WK_ERR_HIP: return "WK_ERR_HIP";
     case WK_ERR_NO_MEMORY: return "WK_ERR_NO_MEMORY";
     case WK_ERR_UNSUPPORTED: return "WK_ERR_UNSUPPORTED";
+    case WK_ERR_DEVICE: return "WK_ERR_DEVICE";
   }
   return "WK_ERR_UNKNOWN";
 }
@@ -84,20 +95,29 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
   if (cfg->device < 0 || cfg->device >= ndev) return invalid("wk_create: device ordinal out of range");
-  wk_handle* h = (wk_handle*)calloc(1, sizeof(wk_handle));
+  wk_handle* h = new (std::nothrow) wk_handle();
   if (!h) return WK_ERR_NO_MEMORY;
   h->cfg = *cfg;
   {
     const char* u = getenv("WAKEWORD_UNFUSED");
     h->unfused = u && u[0] == '1';
+#ifdef WK_DEBUG_EXPERIMENTS
     const char* fx = getenv("WAKEWORD_FUSED_EXP");
     h->fused_exp = fx ? atoi(fx) : 0;
+#endif
   }
   wk_status st = on_device(cfg->device, [&]() -> wk_status {
     hipDeviceProp_t prop;
     hipError_t e2 = hipGetDeviceProperties(&prop, cfg->device);
     if (e2 != hipSuccess) return hip_fail(e2, "hipGetDeviceProperties");
     h->n_cu = prop.multiProcessorCount;
+    if ((e2 = hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+      return hip_fail(e2, "hipHostMalloc(error word)");
+    *h->h_err = 0;
+    if ((e2 = hipHostGetDevicePointer((void**)&h->d_err, h->h_err, 0)) != hipSuccess)
+      return hip_fail(e2, "hipHostGetDevicePointer(error word)");
+    if ((e2 = hipEventCreateWithFlags(&h->ws_free, hipEventDisableTiming)) != hipSuccess)
+      return hip_fail(e2, "hipEventCreate");
     if (host_weights) {
       if ((e2 = hipMalloc(&h->d_weights, sizeof(float) * WK_NUM_WEIGHTS)) != hipSuccess)
         return hip_fail(e2, "hipMalloc(weights)");
@@ -149,10 +169,30 @@ wk_status wk_destroy(wk_handle* h) {
     if (h->d_packed) (void)hipFree(h->d_packed);
     if (h->d_int8) (void)hipFree(h->d_int8);
     if (h->d_bf16) (void)hipFree(h->d_bf16);
+    if (h->ws_free) {
+      (void)hipEventSynchronize(h->ws_free);
+      (void)hipEventDestroy(h->ws_free);
+    }
+    if (h->h_err) (void)hipHostFree(h->h_err);
     return WK_OK;
   });
-  free(h);
+  delete h;
   return WK_OK;
+}
+
+wk_status wk_check_device_errors(wk_handle* h, uint32_t* flags_out) {
+  if (!h) return invalid("wk_check_device_errors: null handle");
+  return on_device(h->cfg.device, [&]() -> wk_status {
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return hip_fail(e, "wk_check_device_errors: sync");
+    const uint32_t f = __atomic_exchange_n(h->h_err, 0u, __ATOMIC_SEQ_CST);
+    if (flags_out) *flags_out = f;
+    if (f) {
+      g_last_error = "fused kernel protocol error (flags " + std::to_string(f) + "): logits since the last check are invalid";
+      return WK_ERR_DEVICE;
+    }
+    return WK_OK;
+  });
 }
 
 static wk_status check_audio(const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len, int64_t clip_stride,
@@ -213,10 +253,19 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
     if ((!h->unfused && !int8) || h->d_bf16) {   // bf16 convolutions exist only in the fused kernel
       const int conv_mode = h->cfg.precision == WK_PREC_BF16 ? 1 : (h->cfg.precision == WK_PREC_BF16X3 ? 2 : 0);
       hipError_t e = wk::launch_fused(dtype == WK_DTYPE_I16, d_audio, batch, clip_stride, h->d_packed, h->d_bf16,
-                                      conv_mode, d_logits, d_feats_or_null, h->n_cu, (hipStream_t)stream, h->fused_exp);
+                                      conv_mode, d_logits, d_feats_or_null, h->n_cu, (hipStream_t)stream, h->d_err,
+                                      h->fused_exp);
       return e == hipSuccess ? WK_OK : hip_fail(e, "fused launch");
     }
     const size_t esz = dtype == WK_DTYPE_I16 ? 2 : 4;
+    // Features staged in the shared workspace: order this use after the last
+    // one, whatever stream it ran on (a caller-provided feature buffer needs no ordering).
+    std::unique_lock<std::mutex> ws_lock(h->ws_mu, std::defer_lock);
+    if (!d_feats_or_null && batch > 0) {
+      ws_lock.lock();
+      hipError_t e = h->ws_used ? hipStreamWaitEvent((hipStream_t)stream, h->ws_free, 0) : hipSuccess;
+      if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent(workspace)");
+    }
     for (int64_t c0 = 0; c0 < batch; c0 += h->ws_clips) {
       const int64_t n = batch - c0 < h->ws_clips ? batch - c0 : h->ws_clips;
       float* feats = d_feats_or_null ? d_feats_or_null + c0 * 13 * 63 : h->d_feats_ws;
@@ -227,6 +276,11 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
       e = int8 ? wk::launch_int8_cnn(feats, n, h->d_int8, d_logits + c0, 4 * h->n_cu, (hipStream_t)stream)
                : wk::launch_cnn(feats, n, h->d_weights, d_logits + c0, false, h->n_cu, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(e, "cnn launch");
+    }
+    if (ws_lock.owns_lock()) {
+      hipError_t e = hipEventRecord(h->ws_free, (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(e, "hipEventRecord(workspace)");
+      h->ws_used = true;
     }
     return WK_OK;
   });
@@ -516,6 +570,10 @@ wk_status wk_stream_push(wk_stream* s, const float* samples, int64_t n, float* o
             hipSuccess ||
         (e = hipStreamSynchronize(s->st)) != hipSuccess)
       return hip_fail(e, "wk_stream_push: D2H");
+    if (const uint32_t f = __atomic_exchange_n(s->h->h_err, 0u, __ATOMIC_SEQ_CST)) {   // synced: the word is final
+      g_last_error = "fused kernel protocol error (flags " + std::to_string(f) + "): these logits are invalid";
+      return WK_ERR_DEVICE;
+    }
     memcpy(out_logits, s->h_logits, sizeof(float) * (size_t)k);
     if (out_end)
       for (int64_t i = 0; i < k; ++i) out_end[i] = (first + i) * s->hop + WK_WIN_SAMPLES;

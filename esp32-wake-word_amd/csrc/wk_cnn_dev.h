@@ -65,11 +65,33 @@ __device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g,
   }
 }
 
-// ---- bf16 convolutions (v_mfma_f32_16x16x16_bf16; WK_PREC_BF16) ----------
-typedef short s4 __attribute__((ext_vector_type(4)));
+// ---- bf16 convolutions (WK_PREC_BF16 / BF16X3) -----------------------------
+// Fragments hold 8 bf16 per lane (K = 32 per step): one 16-byte LDS read per
+// B fragment and one 16-byte load per A fragment.  A step is issued as two
+// CDNA3-era v_mfma_f32_16x16x16_bf16 (elements 0-3, then 4-7 of each lane).
+// gfx950's single-instruction K=32 form (v_mfma_f32_16x16x32_bf16, -DWK_MFMA_K32)
+// is the same work in the same ~16 cycles as ONE K=16 instruction
+// (tools/debug/mfma_rate.hip), but in this kernel it corrupted the front-end:
+// with it on the CNN waves, ~14 % of full-size launches' clips came out with
+// a few power bins of one frame wrong, always in lanes 48-63 of a front-end
+// wave (frames 48-62; tools/debug/logmel_probe.py on a -DWK_DEBUG_LOGMEL
+// build), non-deterministically.  Padding every instruction with s_nop, keeping
+// MFMA destinations off their sources, or slowing the CNN 3x did not remove
+// it; the two-instruction form did (bit-identical repeats at 65,536 clips).
+// The K=32 form measured only +1-3 % end to end (the front-end dominates).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s8 __attribute__((ext_vector_type(8)));   // one lane's A or B fragment: 8 bf16 bit patterns
 
-__device__ __forceinline__ f32x4 mfma_bf16(s4 a, s4 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma_bf16(s8 a, s8 b, f32x4 c) {
+#ifdef WK_MFMA_K32
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+#else
+  c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 0, 1, 2, 3),
+                                                __builtin_shufflevector(b, b, 0, 1, 2, 3), c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 4, 5, 6, 7),
+                                                   __builtin_shufflevector(b, b, 4, 5, 6, 7), c, 0, 0, 0);
+#endif
 }
 
 __device__ __forceinline__ uint32_t bf16_bits(float x) {   // round to nearest even
@@ -77,17 +99,33 @@ __device__ __forceinline__ uint32_t bf16_bits(float x) {   // round to nearest e
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }
 
+// K order of the fragments (wk_kernels.h pack_fragments_bf16): lane group
+// g = lane >> 4 feeds k = 32 s + 8 g + j (j = 0..7) at step s, k = tap * CINP +
+// ci, so its 8 B values are 8 consecutive ci of one image row: one 16-byte
+// read.  kofs = that read's element offset from the lane's t row.  CINP = 16
+// (conv1): step 0 = taps 0, 1; step 1 = tap 2 in groups 0-1 and K padding in
+// groups 2-3, whose weights are zero and whose B read re-reads tap 2 (finite
+// data: 0 * NaN garbage would poison the accumulator).
+template <int CINP, int CIP>
+__device__ __forceinline__ int kofs(int s, int g) {
+  if constexpr (CINP >= 32) {
+    return ((32 * s) / CINP) * CIP + (32 * s) % CINP + 8 * g;
+  } else {
+    const int tap = 2 * s + (g >> 1);
+    return (tap < 2 ? tap : 2) * CIP + 8 * (g & 1);
+  }
+}
+
 // Two 16-column t-tiles of one conv layer from a bf16 [clip][t][ci] image
-// (ci pitch CIP).  Step s covers k = 16s..16s+15 = (tap = s / CB, ci block
-// s % CB); boff = this lane's element offset (t row + 4 (lane >> 4)).
-template <int NSTEP, int CB, int CIP, int CHUNK = 0>
-__device__ __forceinline__ void conv_pair_bf(const uint16_t* __restrict__ img, const s4 (&wf)[NSTEP], int boff_a,
-                                             int boff_b, f32x4& acc_a, f32x4& acc_b) {
+// (ci pitch CIP).  boff = this lane's t row (element offset), g = lane >> 4.
+template <int NSTEP, int CINP, int CIP, int CHUNK = 0>
+__device__ __forceinline__ void conv_pair_bf(const uint16_t* __restrict__ img, const s8 (&wf)[NSTEP], int boff_a,
+                                             int boff_b, int g, f32x4& acc_a, f32x4& acc_b) {
 #pragma unroll
   for (int s = 0; s < NSTEP; ++s) {
-    const int off = (s / CB) * CIP + 16 * (s % CB);
-    const s4 ba = *reinterpret_cast<const s4*>(img + boff_a + off);
-    const s4 bb = *reinterpret_cast<const s4*>(img + boff_b + off);
+    const int off = kofs<CINP, CIP>(s, g);
+    const s8 ba = *reinterpret_cast<const s8*>(img + boff_a + off);
+    const s8 bb = *reinterpret_cast<const s8*>(img + boff_b + off);
     acc_a = mfma_bf16(wf[s], ba, acc_a);
     acc_b = mfma_bf16(wf[s], bb, acc_b);
     if (CHUNK > 0 && (s % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
@@ -119,24 +157,21 @@ __device__ __forceinline__ void epi_pool_bf(const f32x4& acc, uint16_t* __restri
 // x = xh + xl and w = wh + wl with xh = bf16(x), xl = bf16(x - xh) (both RNE);
 // x w ~= xh wh + (xl wh + xh wl), dropping xl wl (relative 2^-16).  Each bf16
 // product is exact in the fp32 accumulator, so the per-product error is
-// ~2^-16 relative -- three v_mfma_f32_16x16x16_bf16 (8 passes each) in place
-// of four v_mfma_f32_16x16x4f32 (fp32 MFMA: 1/16 the bf16 rate).  Images hold
-// xh at ci and xl at ci + LO (LO = 16 CB) of the same t row.  All three
-// products chain on one accumulator per tile (no VALU sum of partial
-// accumulators in the epilogue; measured faster than separate cross-term
-// accumulators).
-template <int NSTEP, int CB, int CIP, int CHUNK = 0>
-__device__ __forceinline__ void conv_pair_bf3(const uint16_t* __restrict__ img, const s4 (&wh)[NSTEP],
-                                              const s4 (&wl)[NSTEP], int boff_a, int boff_b, f32x4& acc_a,
+// ~2^-16 relative -- three K=32 bf16 steps (mfma_bf16) in place of eight
+// v_mfma_f32_16x16x4f32 (fp32 MFMA: 1/16 the bf16 rate).  Images hold
+// xh at ci and xl at ci + CINP of the same t row.  All three products chain on
+// one accumulator per tile (no VALU sum of partial accumulators).
+template <int NSTEP, int CINP, int CIP, int CHUNK = 0>
+__device__ __forceinline__ void conv_pair_bf3(const uint16_t* __restrict__ img, const s8 (&wh)[NSTEP],
+                                              const s8 (&wl)[NSTEP], int boff_a, int boff_b, int g, f32x4& acc_a,
                                               f32x4& acc_b) {
-  constexpr int LO = 16 * CB;
 #pragma unroll
   for (int s = 0; s < NSTEP; ++s) {
-    const int off = (s / CB) * CIP + 16 * (s % CB);
-    const s4 ha = *reinterpret_cast<const s4*>(img + boff_a + off);
-    const s4 hb = *reinterpret_cast<const s4*>(img + boff_b + off);
-    const s4 la = *reinterpret_cast<const s4*>(img + boff_a + off + LO);
-    const s4 lb = *reinterpret_cast<const s4*>(img + boff_b + off + LO);
+    const int off = kofs<CINP, CIP>(s, g);
+    const s8 ha = *reinterpret_cast<const s8*>(img + boff_a + off);
+    const s8 hb = *reinterpret_cast<const s8*>(img + boff_b + off);
+    const s8 la = *reinterpret_cast<const s8*>(img + boff_a + off + CINP);
+    const s8 lb = *reinterpret_cast<const s8*>(img + boff_b + off + CINP);
     acc_a = mfma_bf16(wl[s], ha, acc_a);
     acc_b = mfma_bf16(wl[s], hb, acc_b);
     acc_a = mfma_bf16(wh[s], la, acc_a);

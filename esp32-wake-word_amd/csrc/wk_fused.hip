@@ -40,6 +40,17 @@ __device__ unsigned long long g_wk_stamps[16][16];
 #define WK_SP_ARG
 #endif
 
+#ifdef WK_DEBUG_LOGMEL
+// Diagnostic build only: the log-mel image of every clip as the front-end
+// left it and as the DCT read it, [clip][40][64] each.
+__device__ float* g_dbg_fe;
+__device__ float* g_dbg_cnn;
+__device__ __forceinline__ void dbg_copy_logmel(float* dst, const float* lbuf, int64_t clip, int lane) {
+  if (!dst) return;
+  for (int m = 0; m < 40; ++m) dst[(clip * 40 + m) * 64 + lane] = lbuf[m * WK_LSTRIDE + lane];
+}
+#endif
+
 constexpr int NBF = 4;               // clips per CNN batch
 #ifndef WK_FE_TWS
 #define WK_FE_TWS 1                  // real-FFT split with the combined twiddle table (fe_rest TWS)
@@ -250,6 +261,9 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       if (r == 0) {
         spin_until(ctrl, kCtrlFeBar, p_wait);   // every wave done reading clip i-1's power rows
         WK_STAMP(9);
+#ifdef WK_DEBUG_LOGMEL
+        if (wave == 0 && i >= 1) dbg_copy_logmel(g_dbg_fe, (i - 1) & 1 ? L1 : L, clip_of(i - 1), lane);
+#endif
       }
       float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
       fe_rest<true, decltype(pf_part), (bool)WK_FE_TWS>(a, j, lane, row, tb, w512, 0, pf_part WK_SP_ARG);
@@ -388,8 +402,8 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   constexpr bool BF = CM == kConvBf16, X3 = CM == kConvBf16x3;
   constexpr int kLoW = kNumPackedBf16;   // the xl fragments follow the xh ones (pack_fragments_bf16x3)
   const auto rsb = make_rsrc(pkb, 2 * kNumPackedBf16 * (X3 ? 2 : 1));
-  auto frag_bf = [&](int elem_off) -> s4 {   // one lane's 4 bf16 of the fragment at elem_off (x 64 lanes x 4)
-    return __builtin_bit_cast(s4, __builtin_amdgcn_raw_buffer_load_b64(rsb, 8 * lane, 2 * elem_off, 0));
+  auto frag_bf = [&](int elem_off) -> s8 {   // one lane's 8 bf16 of the fragment at elem_off (x 64 lanes x 8)
+    return __builtin_bit_cast(s8, __builtin_amdgcn_raw_buffer_load_b128(rsb, 16 * lane, 2 * elem_off, 0));
   };
   float* Gp = smem + kGOff;
   float* FCP = smem + kFcpOff;
@@ -404,10 +418,10 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   // 256-byte load per A fragment.  conv3's (48 fragments) stay in VGPRs; the
   // other layers' are re-read from L2 per batch.
   float w3[48];
-  s4 w3b[12];
+  s8 w3b[6];
   if constexpr (BF || X3) {
 #pragma unroll
-    for (int s = 0; s < 12; ++s) w3b[s] = frag_bf(kPbW3 + (cw * 12 + s) * 256);
+    for (int s = 0; s < 6; ++s) w3b[s] = frag_bf(kPbW3 + (cw * 6 + s) * kBfFrag);
   }
 #ifndef WK_W3_RESIDENT
 #define WK_W3_RESIDENT 1   // fp32 conv3 taps: in VGPRs across batches (1), re-read from L2 per pass (0), or loaded
@@ -427,6 +441,9 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   bool eager_done = false;
   auto dct_clip = [&](int64_t i, int slot) {
     float* fo = FEATS ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) : nullptr;
+#ifdef WK_DEBUG_LOGMEL
+    dbg_copy_logmel(g_dbg_cnn, i & 1 ? L1 : L, (int64_t)blockIdx.x + G * i, lane);
+#endif
     dct_cmvn_clip<CM>(i & 1 ? L1 : L, slot, F0, B0, X0, fo, lane);
     signal_set(ctrl, kCtrlLFree + cw, (unsigned)(i + NBF), lane);
   };
@@ -460,14 +477,14 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     eager_done = false;
     // conv1's A fragments: loaded after the DCT (register pressure), landing during the sync.
     float w1[12];
-    s4 w1b[3], w1l[3];
+    s8 w1b[2], w1l[2];
     if constexpr (BF || X3) {
 #pragma unroll
-      for (int s = 0; s < 3; ++s) w1b[s] = frag_bf(kPbW1 + ((cw & 1) * 3 + s) * 256);
+      for (int s = 0; s < 2; ++s) w1b[s] = frag_bf(kPbW1 + ((cw & 1) * 2 + s) * kBfFrag);
     }
     if constexpr (X3) {
 #pragma unroll
-      for (int s = 0; s < 3; ++s) w1l[s] = frag_bf(kLoW + kPbW1 + ((cw & 1) * 3 + s) * 256);
+      for (int s = 0; s < 2; ++s) w1l[s] = frag_bf(kLoW + kPbW1 + ((cw & 1) * 2 + s) * kBfFrag);
     }
     if constexpr (CM == kConvF32) {
 #pragma unroll
@@ -479,18 +496,18 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     // conv1: co tile (cw&1), clip (cw>>1), 4 t-tiles.
     {
       const int co0 = 16 * (cw & 1), cl = cw >> 1;
-      const int bo = (cl * I0_TP + li) * I0_CIP + 4 * lk;   // this lane's element in the [clip][t][ci] image
+      const int bo = (cl * I0_TP + li) * I0_CIP;   // this lane's t row in the bf16 [clip][t][ci] image
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int ta = 32 * p, tb = ta + 16;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
         if constexpr (BF) {
-          conv_pair_bf<3, 1, I0_CIP>(B0, w1b, bo + ta * I0_CIP, bo + tb * I0_CIP, acc_a, acc_b);
+          conv_pair_bf<2, 16, I0_CIP>(B0, w1b, bo + ta * I0_CIP, bo + tb * I0_CIP, lk, acc_a, acc_b);
           epi_pool_bf<I1_CIP, I1_TP, 31>(acc_a, B1, co0, cl, ta, lane);
           epi_pool_bf<I1_CIP, I1_TP, 31>(acc_b, B1, co0, cl, tb, lane);
         } else if constexpr (X3) {
-          const int bx = (cl * I0_TP + li) * X0_CIP + 4 * lk;
-          conv_pair_bf3<3, 1, X0_CIP>(X0, w1b, w1l, bx + ta * X0_CIP, bx + tb * X0_CIP, acc_a, acc_b);
+          const int bx = (cl * I0_TP + li) * X0_CIP;
+          conv_pair_bf3<2, 16, X0_CIP>(X0, w1b, w1l, bx + ta * X0_CIP, bx + tb * X0_CIP, lk, acc_a, acc_b);
           epi_pool_bf3<X1_CIP, I1_TP, 31, 32>(acc_a, X1, co0, cl, ta, lane);
           epi_pool_bf3<X1_CIP, I1_TP, 31, 32>(acc_b, X1, co0, cl, tb, lane);
         } else {
@@ -508,32 +525,32 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
 
     // conv2: co tile (cw&3), clips 2*(cw>>2) + {0,1}, 2 t-tiles each.
     if constexpr (BF) {
-      s4 w2b[6];
+      s8 w2b[3];
 #pragma unroll
-      for (int s = 0; s < 6; ++s) w2b[s] = frag_bf(kPbW2 + ((cw & 3) * 6 + s) * 256);
+      for (int s = 0; s < 3; ++s) w2b[s] = frag_bf(kPbW2 + ((cw & 3) * 3 + s) * kBfFrag);
       const int co0 = 16 * (cw & 3);
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
-        const int bb = (cl * I1_TP + li) * I1_CIP + 4 * lk;
+        const int bb = (cl * I1_TP + li) * I1_CIP;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
-        conv_pair_bf<6, 2, I1_CIP>(B1, w2b, bb, bb + 16 * I1_CIP, acc_a, acc_b);
+        conv_pair_bf<3, 32, I1_CIP>(B1, w2b, bb, bb + 16 * I1_CIP, lk, acc_a, acc_b);
         epi_pool_bf<I2_CIP, I2_TP, 15>(acc_a, B2, co0, cl, 0, lane);
         epi_pool_bf<I2_CIP, I2_TP, 15>(acc_b, B2, co0, cl, 16, lane);
       }
     } else if constexpr (X3) {
-      s4 w2b[6], w2l[6];
+      s8 w2b[3], w2l[3];
 #pragma unroll
-      for (int s = 0; s < 6; ++s) w2b[s] = frag_bf(kPbW2 + ((cw & 3) * 6 + s) * 256);
+      for (int s = 0; s < 3; ++s) w2b[s] = frag_bf(kPbW2 + ((cw & 3) * 3 + s) * kBfFrag);
 #pragma unroll
-      for (int s = 0; s < 6; ++s) w2l[s] = frag_bf(kLoW + kPbW2 + ((cw & 3) * 6 + s) * 256);
+      for (int s = 0; s < 3; ++s) w2l[s] = frag_bf(kLoW + kPbW2 + ((cw & 3) * 3 + s) * kBfFrag);
       const int co0 = 16 * (cw & 3);
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
-        const int bb = (cl * I1_TP + li) * X1_CIP + 4 * lk;
+        const int bb = (cl * I1_TP + li) * X1_CIP;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
-        conv_pair_bf3<6, 2, X1_CIP>(X1, w2b, w2l, bb, bb + 16 * X1_CIP, acc_a, acc_b);
+        conv_pair_bf3<3, 32, X1_CIP>(X1, w2b, w2l, bb, bb + 16 * X1_CIP, lk, acc_a, acc_b);
         epi_pool_bf3<X2_CIP, I2_TP, 15, 64>(acc_a, X2, co0, cl, 0, lane);
         epi_pool_bf3<X2_CIP, I2_TP, 15, 64>(acc_b, X2, co0, cl, 16, lane);
       }
@@ -562,20 +579,21 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     // conv3: co tile cw, the 4 clips; GAP -> G[128][4].
     {
       const int co0 = 16 * cw;
-      const int bo = li * I2_CIP + 4 * lk;
+      const int bo = li * I2_CIP;
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int ca = 2 * p, cb = 2 * p + 1;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
         if constexpr (BF) {
-          conv_pair_bf<12, 4, I2_CIP, 6>(B2, w3b, bo + ca * I2_TP * I2_CIP, bo + cb * I2_TP * I2_CIP, acc_a, acc_b);
+          conv_pair_bf<6, 64, I2_CIP, 3>(B2, w3b, bo + ca * I2_TP * I2_CIP, bo + cb * I2_TP * I2_CIP, lk, acc_a,
+                                         acc_b);
         } else if constexpr (X3) {
-          s4 w3l[12];   // the lo parts are re-read from L2 per pass (VGPR budget)
+          s8 w3l[6];   // the lo parts are re-read from L2 per pass (VGPR budget)
 #pragma unroll
-          for (int s = 0; s < 12; ++s) w3l[s] = frag_bf(kLoW + kPbW3 + (cw * 12 + s) * 256);
-          const int bx = li * X2_CIP + 4 * lk;
-          conv_pair_bf3<12, 4, X2_CIP, 3>(X2, w3b, w3l, bx + ca * I2_TP * X2_CIP, bx + cb * I2_TP * X2_CIP, acc_a,
-                                          acc_b);
+          for (int s = 0; s < 6; ++s) w3l[s] = frag_bf(kLoW + kPbW3 + (cw * 6 + s) * kBfFrag);
+          const int bx = li * X2_CIP;
+          conv_pair_bf3<6, 64, X2_CIP, 2>(X2, w3b, w3l, bx + ca * I2_TP * X2_CIP, bx + cb * I2_TP * X2_CIP, lk,
+                                          acc_a, acc_b);
         } else {
           // Winograd: one tile of 16 pair columns = 8 pairs of clip ca, 8 of clip cb
           if (!WK_W3_RESIDENT) {
@@ -654,7 +672,8 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
                                                                  int64_t clip_stride, const float* __restrict__ wts,
                                                                  const uint16_t* __restrict__ wbf,
                                                                  float* __restrict__ logits,
-                                                                 float* __restrict__ feats_out, int exp_flags) {
+                                                                 float* __restrict__ feats_out, unsigned* err,
+                                                                 int exp_flags) {
   __shared__ __attribute__((aligned(16))) float smem[kFusedLds];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -673,9 +692,26 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
     if (!(exp_flags & 1)) cnn_role<CM, FEATS>(smem, wts, wbf, n_mine, logits, feats_out, wave - 8, lane, exp_flags);
 #endif
   }
+  // Protocol health: a spin that timed out set the workgroup's abort word, and
+  // every logit of this launch is then suspect.  Each wave reports what it
+  // sees on exit to the handle's error word (host-visible; read by
+  // wk_check_device_errors / wk_stream_push): bit 0 = a spin timed out, bit 1 =
+  // the abort word holds a value no spin writes (LDS corruption).
+  if (lane == 0 && err) {
+    const unsigned ab = lds_load(reinterpret_cast<unsigned*>(smem + kCtrlOff) + kCtrlAbort);
+    if (ab) __hip_atomic_store(err, ab == 1u ? 1u : 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 }  // namespace
+
+#ifdef WK_DEBUG_LOGMEL
+extern "C" int wk_debug_logmel_set(float* fe, float* cnn) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_fe), &fe, sizeof(fe)) != hipSuccess) return 1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_cnn), &cnn, sizeof(cnn)) != hipSuccess) return 1;
+  return 0;
+}
+#endif
 
 #ifdef WK_STAMPS
 extern "C" int wk_debug_stamps(unsigned long long* host_out, int reset) {
@@ -692,7 +728,7 @@ namespace wk {
 
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
                         const uint16_t* wbf, int conv_mode, float* logits, float* feats_or_null, int grid_cap,
-                        hipStream_t stream, int exp_flags) {
+                        hipStream_t stream, unsigned* err, int exp_flags) {
   if (batch == 0) return hipSuccess;
   const int grid = (int)(batch < grid_cap ? batch : grid_cap);
   const dim3 g(grid), blk(kFusedBlock);
@@ -701,10 +737,10 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
   do {                                                                                                         \
     if (feats_or_null)                                                                                         \
       hipLaunchKernelGGL((wk_fused_kernel<T, CM, true>), g, blk, 0, stream, (const T*)audio, batch, clip_stride, \
-                         w, wbf, logits, feats_or_null, exp_flags);                                            \
+                         w, wbf, logits, feats_or_null, err, exp_flags);                                            \
     else                                                                                                       \
       hipLaunchKernelGGL((wk_fused_kernel<T, CM, false>), g, blk, 0, stream, (const T*)audio, batch,            \
-                         clip_stride, w, wbf, logits, nullptr, exp_flags);                                     \
+                         clip_stride, w, wbf, logits, nullptr, err, exp_flags);                                     \
   } while (0)
   if (i16) {
     if (conv_mode == kConvBf16) WK_FUSED_LAUNCH(int16_t, kConvBf16);

@@ -46,7 +46,9 @@ hipError_t launch_cnn(const float* feats, int64_t batch, const float* w, float* 
 // (bf16, config 4) and 2 (split bf16, WK_PREC_BF16X3); conv_mode 0 = fp32 MFMA.
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
                         const uint16_t* wbf, int conv_mode, float* logits, float* feats_or_null, int grid_cap, hipStream_t stream,
-                        int exp_flags = 0);   // exp_flags (timing experiments only): 1 = FE role only, 2 = CNN only
+                        unsigned* err,        // host-visible protocol error word (see wk_fused_kernel), may be null
+                        int exp_flags = 0);   // timing experiments (-DWK_DEBUG_EXPERIMENTS builds only): 1 = FE role
+                                              // only, 2 = CNN role only; wrong logits
 
 // int8 CNN in the device's esp-dl arithmetic (wk_int8.hip); feats [B][13][63] fp32.
 constexpr int kNumInt8Weights = 3 * 13 * 32 + 3 * 32 * 64 + 3 * 64 * 128 + 128 * 64 + 64;
@@ -84,14 +86,15 @@ constexpr int kPkF1 = kPkW3 + 8 * 48 * 64;      // [4 o-tiles][32 s][64]  (k = 4
 constexpr int kPkF2 = kPkF1 + 4 * 32 * 64;      // [64]
 constexpr int kNumPacked = kPkF2 + 64;
 
-// bf16 variant (WK_PREC_BF16, v_mfma_f32_16x16x16_bf16): per 16-row tile and
-// k-step s (k = 16s..16s+15), lane l feeds 4 consecutive k = 16s + 4(l>>4) + j
-// (j = 0..3) of row l&15 -- one 8-byte load per fragment.  k = tap*Cin_pad + ci.
-// Offsets in bf16 (uint16) units.
-constexpr int kPbW1 = 0;                        // [2 tiles][3 s][64][4]   (Cin 13 padded to 16)
-constexpr int kPbW2 = kPbW1 + 2 * 3 * 64 * 4;   // [4][6][64][4]
-constexpr int kPbW3 = kPbW2 + 4 * 6 * 64 * 4;   // [8][12][64][4]
-constexpr int kNumPackedBf16 = kPbW3 + 8 * 12 * 64 * 4;
+// bf16 variant (WK_PREC_BF16 / BF16X3, v_mfma_f32_16x16x32_bf16): per 16-row
+// tile and k-step s, lane l feeds 8 consecutive k = 32s + 8(l>>4) + j (j = 0..7)
+// of row l&15 -- one 16-byte load per fragment.  k = tap*Cin_pad + ci, zero
+// past 3*Cin_pad (conv1: 48 -> 2 steps).  Offsets in bf16 (uint16) units.
+constexpr int kPbW1 = 0;                        // [2 tiles][2 s][64][8]   (Cin 13 padded to 16)
+constexpr int kPbW2 = kPbW1 + 2 * 2 * 64 * 8;   // [4][3][64][8]
+constexpr int kPbW3 = kPbW2 + 4 * 3 * 64 * 8;   // [8][6][64][8]
+constexpr int kNumPackedBf16 = kPbW3 + 8 * 6 * 64 * 8;
+constexpr int kBfFrag = 64 * 8;                 // bf16 elements per fragment
 
 inline uint16_t to_bf16_rne(float x) {
   uint32_t u;
@@ -112,14 +115,14 @@ inline uint16_t split_bf16(float x, bool lo) {
 
 inline void pack_fragments_bf16(const float* w, uint16_t* pk, bool lo = false) {
   auto pack = [&](int off, int cout_tiles, int cin, int cin_pad, int wbase) {
-    const int nsteps = 3 * cin_pad / 16;
+    const int nsteps = (3 * cin_pad + 31) / 32;
     for (int t = 0; t < cout_tiles; ++t)
       for (int s = 0; s < nsteps; ++s)
         for (int l = 0; l < 64; ++l)
-          for (int j = 0; j < 4; ++j) {
-            const int co = 16 * t + (l & 15), k = 16 * s + 4 * (l >> 4) + j, tap = k / cin_pad, ci = k % cin_pad;
-            pk[off + ((t * nsteps + s) * 64 + l) * 4 + j] =
-                ci < cin ? split_bf16(w[wbase + (co * cin + ci) * 3 + tap], lo) : (uint16_t)0;
+          for (int j = 0; j < 8; ++j) {
+            const int co = 16 * t + (l & 15), k = 32 * s + 8 * (l >> 4) + j, tap = k / cin_pad, ci = k % cin_pad;
+            pk[off + ((t * nsteps + s) * 64 + l) * 8 + j] =
+                tap < 3 && ci < cin ? split_bf16(w[wbase + (co * cin + ci) * 3 + tap], lo) : (uint16_t)0;
           }
   };
   pack(kPbW1, 2, 13, 16, kOffW1);

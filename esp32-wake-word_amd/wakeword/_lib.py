@@ -29,7 +29,8 @@ EXPORTS = ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_syn
            "wk_status_string", "wk_last_error", "wk_abi_version", "extract_mfcc", "free_mfcc",
            "analyze_mfcc_range", "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push",
            "wk_ctc_num_weights", "wk_ctc_create", "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward",
-           "wk_wav_read", "wk_wav_load_batch", "wk_augment", "flow_extract_mfcc_single_frame", "wk_device_cmvn")
+           "wk_wav_read", "wk_wav_load_batch", "wk_augment", "flow_extract_mfcc_single_frame", "wk_device_cmvn",
+           "wk_check_device_errors")
 
 
 class WkConfig(C.Structure):
@@ -88,6 +89,7 @@ def _declare(L):
     L.wk_wav_load_batch.argtypes = [C.POINTER(C.c_char_p), i32, i32, C.c_float, u32, vp, vp]
     L.wk_augment.argtypes = [vp, i32, C.c_float, C.c_float, C.c_float, u32, vp, i32]
     L.wk_device_cmvn.argtypes = [vp, i32, i64, vp, vp, vp]
+    L.wk_check_device_errors.argtypes = [vp, C.POINTER(u32)]
     for name in ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_synth_clips", "wk_normalize",
                  "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push", "wk_ctc_create",
                  "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward", "wk_wav_read", "wk_wav_load_batch",

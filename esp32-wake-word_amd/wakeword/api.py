@@ -227,6 +227,13 @@ class KWSModel:
     def probability(self, audio):
         return _torch().sigmoid(self.detect(audio))
 
+    def check_device_errors(self) -> None:
+        """Synchronise the device and raise WakewordError if a fused launch on
+        this model since the last check reported a role hand-off failure (its
+        logits are then invalid; wk_check_device_errors in include/wakeword.h)."""
+        flags = C.c_uint32(0)
+        check(lib().wk_check_device_errors(self._h.h, C.byref(flags)), "wk_check_device_errors")
+
 
 def load_onnx(path: str, device: int = 0, precision: str = "fp32") -> KWSModel:
     """Load ``xiaoa.onnx`` (ml_models/xiaoa.onnx) into a device-resident KWSModel."""

@@ -34,7 +34,9 @@ typedef enum {
   WK_ERR_INVALID_ARG = 1,   /* null pointer, bad size, unsupported parameter combo */
   WK_ERR_HIP = 2,           /* a HIP runtime call failed (see wk_last_error())     */
   WK_ERR_NO_MEMORY = 3,     /* device or host allocation failed                    */
-  WK_ERR_UNSUPPORTED = 4    /* valid request this build does not implement         */
+  WK_ERR_UNSUPPORTED = 4,   /* valid request this build does not implement         */
+  WK_ERR_DEVICE = 5         /* a kernel reported an internal protocol failure: the */
+                            /* results of the launches it covers are invalid       */
 } wk_status;
 
 /* Front-end definitions. */
@@ -83,6 +85,15 @@ typedef struct wk_handle wk_handle;
 wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle** out);
 wk_status wk_destroy(wk_handle* h);
 
+/* The fused kernel's two roles (front-end waves, CNN waves) hand clips over
+ * through bounded spins; a spin that times out (a protocol failure -- never
+ * expected) ends the launch with invalid logits instead of a hung GPU, and
+ * raises a flag in a host-visible word of the handle.  This call synchronises
+ * the handle's device, returns WK_ERR_DEVICE if any launch on the handle since
+ * the last check raised it (flags in *flags_out, may be NULL; 0 = clean), and
+ * clears it.  wk_stream_push checks the word itself on every push. */
+wk_status wk_check_device_errors(wk_handle* h, uint32_t* flags_out);
+
 /* Front-end only.  d_audio: `batch` clips of `win_len` samples, clip i at
  * d_audio + i*clip_stride elements (dtype WK_DTYPE_F32 or WK_DTYPE_I16; i16 is
  * scaled by 1/32768 like torchaudio.load).  Mode B requires win_len == 16000
@@ -97,7 +108,10 @@ wk_status wk_cnn(wk_handle* h, const float* d_feats, int64_t batch, float* d_log
 
 /* Fused hot path: audio -> logits [batch]; mode B only (the model's training
  * front-end).  d_feats_or_null, when given, receives the [batch][13][63]
- * features as well. */
+ * features as well.  A handle may be used from several streams and host
+ * threads: the INT8 / unfused path stages features in a per-handle workspace
+ * (when d_feats_or_null is NULL) and orders its uses across streams with an
+ * event; the fused path shares nothing between calls. */
 wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len,
                      int64_t clip_stride, float* d_logits, float* d_feats_or_null, void* stream);
 

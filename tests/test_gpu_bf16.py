@@ -1,5 +1,5 @@
 """bf16 mode (WK_PREC_BF16): bf16 convolutions
-(v_mfma_f32_16x16x16_bf16, fp32 accumulation) inside the fused kernel, fp32
+(bf16 MFMA, K = 32 per step, fp32 accumulation) inside the fused kernel, fp32
 front-end and classifier.  Tolerance vs the fp32 reference path: 0.05 in logit
 (bf16 keeps 8 mantissa bits; observed ~1e-2), identical decisions on the
 reference WAVs."""
@@ -103,3 +103,4 @@ def test_fused_repeatable_at_scale(gpu, golden_dir, precision):
     for _ in range(4):
         got = m.detect(x).reshape(-1)
         assert int((got != ref).sum()) == 0
+    m.check_device_errors()

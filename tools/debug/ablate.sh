@@ -1,3 +1,4 @@
+# WAKEWORD_FUSED_EXP needs variants built with -DWK_DEBUG_EXPERIMENTS (the shipped library ignores it).
 cd $GRAFT_REPO_ROOT
 for v in prod ${ABL_VARIANTS:-abl_NODFT abl_NOTW abl_NOTRANS abl_NOSPLIT abl_NOMEL}; do
   if [ $v = prod ]; then L=esp32-wake-word_amd/wakeword/libwakeword.so; else L=esp32-wake-word_amd/build/var_$v/libwakeword.so; fi

@@ -1,5 +1,7 @@
 #!/bin/bash
 # FE-alone (exp 1) and fused timing of ablation variants: bash tools/debug/ablate2.sh v1 v2 ...
+# WAKEWORD_FUSED_EXP is honoured only by libraries built with -DWK_DEBUG_EXPERIMENTS
+# (bash tools/debug/build_variant.sh exp -DWK_DEBUG_EXPERIMENTS; WAKEWORD_LIB=...var_exp/libwakeword.so).
 R=$(cd "$(dirname "$0")/../.." && pwd)
 cd "$R"
 for v in "$@"; do
