@@ -445,26 +445,46 @@ void analyze_mfcc_range(float* mfcc, int size, const char* label) {
 // ---------------------------------------------------------------------------
 // Streaming ring.
 //
-// Device ring of `cap` float samples, stored mirrored (sample p at p % cap
-// and p % cap + cap), so every window of <= cap samples is contiguous and a
-// run of consecutive windows is one strided wk_forward launch.  Writes follow
+// A ring of `cap` float samples, stored mirrored (sample p at p % cap and
+// p % cap + cap), so every window of <= cap samples is contiguous and a run of
+// consecutive windows is one strided wk_forward launch.  Writes follow
 // ring_buffer.c:57-117 (write_rinbuffer): a push longer than the ring keeps
 // only its newest `cap` samples, older data is overwritten.  Window k covers
 // stream samples [k*hop, k*hop + 16000); a push completes every window whose
 // end it reaches; windows whose start was already overwritten are dropped.
+//
+// Latency path (a push that completes a few windows, the real-time case): the
+// ring and the logits live in pinned, mapped host memory, and the fused
+// kernel reads the window straight from the host ring and writes the logit
+// straight into host memory -- one kernel launch and one wait per push, no
+// copy commands.  A push that completes more than kZeroCopyMax windows (a
+// backlog) copies the run's samples to device memory first, so the kernel
+// reads HBM rather than re-reading overlapping windows across PCIe.
 // ---------------------------------------------------------------------------
+namespace {
+constexpr int64_t kZeroCopyMax = 4;
+}
+
 struct wk_stream {
   wk_handle* h;
   hipStream_t st;
   int32_t hop, cap;
   int64_t total;        // samples pushed since create / reset
   int64_t next_win;     // index of the next window to score
-  float* d_ring;        // [2*cap]
-  float* d_logits;      // [max_win]
-  float* h_stage;       // pinned [cap]
-  float* h_logits;      // pinned [max_win]
+  float* h_ring;        // pinned, mapped [2*cap] (written by the host, read by the kernel)
+  float* a_ring;        // device alias of h_ring
+  float* d_stage;       // device [2*cap]: backlog runs are copied here first
+  float* h_logits;      // pinned, mapped [max_win] (written by the kernel)
+  float* a_logits;      // device alias of h_logits
   int32_t max_win;
 };
+
+static void stream_free(wk_stream* s) {
+  (void)hipHostFree(s->h_ring);
+  (void)hipFree(s->d_stage);
+  (void)hipHostFree(s->h_logits);
+  free(s);
+}
 
 wk_status wk_stream_create(wk_handle* h, int32_t hop, int32_t capacity, void* stream, wk_stream** out) {
   if (!h || !out) return invalid("wk_stream_create: null argument");
@@ -480,19 +500,17 @@ wk_status wk_stream_create(wk_handle* h, int32_t hop, int32_t capacity, void* st
     s->hop = hop;
     s->cap = capacity;
     s->max_win = (capacity - WK_WIN_SAMPLES) / hop + 1;
+    const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
     hipError_t e;
-    if ((e = hipMalloc(&s->d_ring, sizeof(float) * 2 * (size_t)capacity)) != hipSuccess ||
-        (e = hipMalloc(&s->d_logits, sizeof(float) * (size_t)s->max_win)) != hipSuccess ||
-        (e = hipHostMalloc(&s->h_stage, sizeof(float) * (size_t)capacity, hipHostMallocDefault)) != hipSuccess ||
-        (e = hipHostMalloc(&s->h_logits, sizeof(float) * (size_t)s->max_win, hipHostMallocDefault)) != hipSuccess ||
-        (e = hipMemsetAsync(s->d_ring, 0, sizeof(float) * 2 * (size_t)capacity, s->st)) != hipSuccess) {
-      (void)hipFree(s->d_ring);
-      (void)hipFree(s->d_logits);
-      (void)hipHostFree(s->h_stage);
-      (void)hipHostFree(s->h_logits);
-      free(s);
+    if ((e = hipHostMalloc(&s->h_ring, sizeof(float) * 2 * (size_t)capacity, mapped)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&s->a_ring, s->h_ring, 0)) != hipSuccess ||
+        (e = hipMalloc(&s->d_stage, sizeof(float) * 2 * (size_t)capacity)) != hipSuccess ||
+        (e = hipHostMalloc(&s->h_logits, sizeof(float) * (size_t)s->max_win, mapped)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&s->a_logits, s->h_logits, 0)) != hipSuccess) {
+      stream_free(s);
       return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_stream_create");
     }
+    memset(s->h_ring, 0, sizeof(float) * 2 * (size_t)capacity);
     *out = s;
     return WK_OK;
   });
@@ -502,11 +520,7 @@ wk_status wk_stream_destroy(wk_stream* s) {
   if (!s) return WK_OK;
   return on_device(s->h->cfg.device, [&]() -> wk_status {
     (void)hipStreamSynchronize(s->st);
-    (void)hipFree(s->d_ring);
-    (void)hipFree(s->d_logits);
-    (void)hipHostFree(s->h_stage);
-    (void)hipHostFree(s->h_logits);
-    free(s);
+    stream_free(s);
     return WK_OK;
   });
 }
@@ -523,53 +537,54 @@ wk_status wk_stream_push(wk_stream* s, const float* samples, int64_t n, float* o
   if (!s || !n_out || n < 0 || (n > 0 && !samples) || max_out < 0 || (max_out > 0 && !out_logits))
     return invalid("wk_stream_push: bad arguments");
   *n_out = 0;
+  // Every push that launches work waits for it before returning, so no kernel
+  // is reading the host ring while it is rewritten here.
+  const int64_t cap = s->cap;
+  // 1. ring write (overwrite-oldest): only the newest `cap` samples of a long push survive.
+  const int64_t skip = n > cap ? n - cap : 0;
+  const int64_t m = n - skip;
+  const int64_t p0 = s->total + skip;
+  for (int64_t done = 0; done < m;) {   // at most two segments (wrap), each written twice (mirror)
+    const int64_t pos = (p0 + done) % cap;
+    const int64_t len = m - done < cap - pos ? m - done : cap - pos;
+    memcpy(s->h_ring + pos, samples + skip + done, sizeof(float) * (size_t)len);
+    memcpy(s->h_ring + pos + cap, samples + skip + done, sizeof(float) * (size_t)len);
+    done += len;
+  }
+  s->total += n;
+  // 2. windows completed by this push whose start is still in the ring.
+  const int64_t last = s->total >= WK_WIN_SAMPLES ? (s->total - WK_WIN_SAMPLES) / s->hop : -1;
+  int64_t first = s->next_win;
+  const int64_t oldest = s->total > cap ? (s->total - cap + s->hop - 1) / s->hop : 0;
+  if (first < oldest) first = oldest;
+  if (last - first + 1 > max_out) first = last - max_out + 1;   // report the newest max_out
+  s->next_win = last + 1 > s->next_win ? last + 1 : s->next_win;
+  const int64_t k = last - first + 1;
+  if (k <= 0) return WK_OK;
   return on_device(s->h->cfg.device, [&]() -> wk_status {
-    hipError_t e = hipStreamSynchronize(s->st);   // the staging buffer may still feed the last push's copy
-    if (e != hipSuccess) return hip_fail(e, "wk_stream_push: sync");
-    const int64_t cap = s->cap;
-    // 1. ring write (overwrite-oldest): only the newest `cap` samples of a long push survive.
-    const int64_t skip = n > cap ? n - cap : 0;
-    const int64_t m = n - skip;
-    if (m > 0) {
-      memcpy(s->h_stage, samples + skip, sizeof(float) * (size_t)m);
-      const int64_t p0 = s->total + skip;
-      int64_t done = 0;
-      while (done < m) {   // at most two segments (wrap), each written twice (mirror)
-        const int64_t pos = (p0 + done) % cap;
-        const int64_t len = m - done < cap - pos ? m - done : cap - pos;
-        for (int mirror = 0; mirror < 2; ++mirror) {
-          e = hipMemcpyAsync(s->d_ring + pos + mirror * cap, s->h_stage + done, sizeof(float) * (size_t)len,
-                             hipMemcpyHostToDevice, s->st);
-          if (e != hipSuccess) return hip_fail(e, "wk_stream_push: H2D");
-        }
-        done += len;
-      }
-    }
-    s->total += n;
-    // 2. windows completed by this push whose start is still in the ring.
-    const int64_t last = s->total >= WK_WIN_SAMPLES ? (s->total - WK_WIN_SAMPLES) / s->hop : -1;
-    int64_t first = s->next_win;
-    const int64_t oldest = s->total > cap ? (s->total - cap + s->hop - 1) / s->hop : 0;
-    if (first < oldest) first = oldest;
-    if (last - first + 1 > max_out) first = last - max_out + 1;   // report the newest max_out
-    s->next_win = last + 1 > s->next_win ? last + 1 : s->next_win;
-    const int64_t k = last - first + 1;
-    if (k <= 0) return WK_OK;
     // 3. score them: contiguous strided runs in the mirrored ring.
+    hipError_t e;
     int64_t w = first;
     while (w <= last) {
       const int64_t off = (w * s->hop) % cap;
       int64_t run = (2 * cap - WK_WIN_SAMPLES - off) / s->hop + 1;   // windows that fit before the mirror end
       if (run > last - w + 1) run = last - w + 1;
-      wk_status st = wk_forward(s->h, s->d_ring + off, WK_DTYPE_F32, run, WK_WIN_SAMPLES, s->hop,
-                                s->d_logits + (w - first), nullptr, s->st);
+      const float* src = s->a_ring + off;
+      if (run > kZeroCopyMax) {   // backlog: one copy of the run's span to HBM, then score from there
+        const int64_t span = (run - 1) * s->hop + WK_WIN_SAMPLES;
+        if ((e = hipMemcpyAsync(s->d_stage, s->h_ring + off, sizeof(float) * (size_t)span, hipMemcpyHostToDevice,
+                                s->st)) != hipSuccess)
+          return hip_fail(e, "wk_stream_push: H2D");
+        src = s->d_stage;
+      }
+      wk_status st = wk_forward(s->h, src, WK_DTYPE_F32, run, WK_WIN_SAMPLES, s->hop, s->a_logits + (w - first),
+                                nullptr, s->st);
       if (st != WK_OK) return st;
+      if (run > kZeroCopyMax && (e = hipStreamSynchronize(s->st)) != hipSuccess)   // d_stage is reused
+        return hip_fail(e, "wk_stream_push: sync");
       w += run;
     }
-    if ((e = hipMemcpyAsync(s->h_logits, s->d_logits, sizeof(float) * (size_t)k, hipMemcpyDeviceToHost, s->st)) !=
-            hipSuccess ||
-        (e = hipStreamSynchronize(s->st)) != hipSuccess)
-      return hip_fail(e, "wk_stream_push: D2H");
+    if ((e = hipStreamSynchronize(s->st)) != hipSuccess) return hip_fail(e, "wk_stream_push: sync");
     if (const uint32_t f = __atomic_exchange_n(s->h->h_err, 0u, __ATOMIC_SEQ_CST)) {   // synced: the word is final
       g_last_error = "fused kernel protocol error (flags " + std::to_string(f) + "): these logits are invalid";
       return WK_ERR_DEVICE;

@@ -177,6 +177,9 @@ struct WkStamps {
 };
 #define WK_SP_PARAM , WkStamps* stp = nullptr
 #define WK_FE_HIT(k) do { if (stp) stp->hit(k); } while (0)
+#elif defined(WK_ASM_MARKS)   // dev builds: phase markers in the -S output (tools/asm_phases.py)
+#define WK_SP_PARAM
+#define WK_FE_HIT(k) asm volatile(";WKMARK fe" #k)
 #else
 #define WK_SP_PARAM
 #define WK_FE_HIT(k) do {} while (0)

@@ -33,6 +33,11 @@ __device__ unsigned long long g_wk_stamps[16][16];
 #define WK_STAMP(k) _stamps.hit(k)
 #define WK_STAMP_FLUSH(w) do { if (lane == 0) for (int _k = 0; _k < 16; ++_k) atomicAdd(&g_wk_stamps[w][_k], _stamps.st[_k]); } while (0)
 #define WK_SP_ARG , &_stamps
+#elif defined(WK_ASM_MARKS)
+#define WK_STAMP_INIT
+#define WK_STAMP(k) asm volatile(";WKMARK st" #k)
+#define WK_STAMP_FLUSH(w) do {} while (0)
+#define WK_SP_ARG
 #else
 #define WK_STAMP_INIT
 #define WK_STAMP(k) do {} while (0)

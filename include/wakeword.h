@@ -138,7 +138,10 @@ wk_status wk_normalize(const float* d_in, float* d_out, int64_t batch, int32_t n
  * newest max_out are scored) with the fused path on the handle's device, and
  * returns their logits and end positions (samples since create/reset) in host
  * memory.  It blocks until the logits are on the host.  Not thread-safe per
- * stream object. */
+ * stream object.  The ring and the logits live in pinned, mapped host memory:
+ * a push that completes up to 4 windows is one kernel launch that reads the
+ * window from the host ring and writes the logits to host memory directly (no
+ * copy commands); larger backlogs are copied to device memory first. */
 typedef struct wk_stream wk_stream;
 wk_status wk_stream_create(wk_handle* h, int32_t hop, int32_t capacity, void* stream, wk_stream** out);
 wk_status wk_stream_destroy(wk_stream* s);

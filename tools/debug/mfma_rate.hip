@@ -42,25 +42,36 @@ __device__ __forceinline__ void mfma_loop(int iters, float seed, float* out) {
   *out = s;
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+// 64 v_fma_f32 per iteration, or (PK) the same 128 flop-lanes as 32 v_pk_fma_f32.
+template <bool PK>
 __device__ __forceinline__ void valu_loop(int iters, float seed, float* out) {
   float a[8];
+  f2 p[4];
   for (int i = 0; i < 8; ++i) a[i] = seed + i;
+  for (int i = 0; i < 4; ++i) p[i] = f2{seed + i, seed - i};
   const float m = 0.999f, c = 1e-4f;
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
+      if constexpr (PK) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = __builtin_fmaf(a[i], m - i * 1e-6f, c);
+        for (int i = 0; i < 4; ++i) p[i] = __builtin_elementwise_fma(p[i], f2{m - i * 1e-6f, m}, f2{c, c});
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = __builtin_fmaf(a[i], m - i * 1e-6f, c);
+      }
     }
   }
   float s = 0;
   for (int i = 0; i < 8; ++i) s += a[i];
+  for (int i = 0; i < 4; ++i) s += p[i].x + p[i].y;
   *out = s;
 }
 
 // Waves 0..4*MW-1: MFMA loop (16 MFMAs per iteration); the rest: VALU loop
 // (64 v_fma_f32 per iteration).  cyc[0] = mean MFMA-wave cycles, cyc[1] = mean VALU-wave cycles (block 0).
-template <int KIND>
+template <int KIND, bool PK>
 __global__ void k(float* out, int m_iters, int v_iters, int mfma_waves, unsigned long long* cyc) {
   const int wave = threadIdx.x >> 6;
   const float seed = threadIdx.x * 1e-3f;
@@ -69,28 +80,28 @@ __global__ void k(float* out, int m_iters, int v_iters, int mfma_waves, unsigned
   if (wave < mfma_waves) {
     if constexpr (KIND != K_NONE) mfma_loop<KIND>(m_iters, seed, o);
   } else {
-    valu_loop(v_iters, seed, o);
+    valu_loop<PK>(v_iters, seed, o);
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) atomicAdd(&cyc[wave < mfma_waves ? 0 : 1], t1 - t0);
 }
 
-template <int KIND>
+template <int KIND, bool PK = false>
 void run(float* out, unsigned long long* cyc, int mw, int vw, int m_iters, int v_iters) {
   const int ncu = 256;
   const int threads = 64 * 4 * (mw + vw);
   unsigned long long h[2] = {0, 0};
   for (int rep = 0; rep < 2; ++rep) {
     hipMemset(cyc, 0, 16);
-    hipLaunchKernelGGL(k<KIND>, dim3(ncu), dim3(threads), 0, 0, out, m_iters, v_iters, 4 * mw, cyc);
+    hipLaunchKernelGGL((k<KIND, PK>), dim3(ncu), dim3(threads), 0, 0, out, m_iters, v_iters, 4 * mw, cyc);
     hipDeviceSynchronize();
   }
   hipMemcpy(h, cyc, 16, hipMemcpyDeviceToHost);
   const double mc = mw ? (double)h[0] / (4 * mw) : 0, vc = vw ? (double)h[1] / (4 * vw) : 0;
   const double n_mfma = (double)m_iters * 16, n_valu = (double)v_iters * 64;
-  printf("%-18s mfma_waves/SIMD=%d valu_waves/SIMD=%d | mfma wave: %9.0f cyc, %6.2f cyc/MFMA/SIMD | valu wave: %9.0f cyc, "
+  printf("%s %-18s mfma_waves/SIMD=%d valu_waves/SIMD=%d | mfma wave: %9.0f cyc, %6.2f cyc/MFMA/SIMD | valu wave: %9.0f cyc, "
          "%5.2f cyc/v_fma/SIMD\n",
-         kName[KIND], mw, vw, mc, mw ? mc / (n_mfma * mw) : 0.0, vc, vw ? vc / (n_valu * vw) : 0.0);
+         PK ? "pk " : "fma", kName[KIND], mw, vw, mc, mw ? mc / (n_mfma * mw) : 0.0, vc, vw ? vc / (n_valu * vw) : 0.0);
 }
 
 int main() {
@@ -99,18 +110,16 @@ int main() {
   hipMalloc(&out, 256 * 1024 * 4);
   hipMalloc(&cyc, 16);
   const int m_iters = 2000, v_iters = 2000;
-  // (1) MFMA alone, 1 wave/SIMD; (2) VALU alone, 2 waves/SIMD; (3) both.
-  run<K_F32>(out, cyc, 1, 0, m_iters, 0);
-  run<K_BF16_K16>(out, cyc, 1, 0, m_iters, 0);
-  run<K_BF16_K32>(out, cyc, 1, 0, m_iters, 0);
-  run<K_F16_K32>(out, cyc, 1, 0, m_iters, 0);
-  run<K_NONE>(out, cyc, 0, 2, 0, v_iters);
-  run<K_F32>(out, cyc, 1, 2, m_iters / 4, v_iters);
-  run<K_BF16_K16>(out, cyc, 1, 2, m_iters, v_iters);
-  run<K_BF16_K32>(out, cyc, 1, 2, m_iters, v_iters);
-  run<K_F16_K32>(out, cyc, 1, 2, m_iters, v_iters);
-  run<K_F32>(out, cyc, 2, 2, m_iters / 4, v_iters);
-  run<K_BF16_K16>(out, cyc, 2, 2, m_iters, v_iters);
-  run<K_BF16_K32>(out, cyc, 2, 2, m_iters, v_iters);
+  // VALU waves alone (2/SIMD), then beside one MFMA wave per SIMD: plain vs packed FMA.
+  run<K_NONE, false>(out, cyc, 0, 2, 0, v_iters);
+  run<K_NONE, true>(out, cyc, 0, 2, 0, v_iters);
+  run<K_F32, false>(out, cyc, 1, 2, m_iters / 4, v_iters);
+  run<K_F32, true>(out, cyc, 1, 2, m_iters / 4, v_iters);
+  run<K_BF16_K16, false>(out, cyc, 1, 2, m_iters, v_iters);
+  run<K_BF16_K16, true>(out, cyc, 1, 2, m_iters, v_iters);
+  run<K_NONE, false>(out, cyc, 0, 1, 0, v_iters);
+  run<K_NONE, true>(out, cyc, 0, 1, 0, v_iters);
+  run<K_F32, false>(out, cyc, 1, 1, m_iters / 4, v_iters);
+  run<K_F32, true>(out, cyc, 1, 1, m_iters / 4, v_iters);
   return 0;
 }
