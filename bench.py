@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--audio", default="f32", choices=["f32", "i16"],
                     help="sample type of the resident clips: f32 (the metric's workload, 64,000 B/window) or "
                          "i16 PCM (32,000 B/window, scaled by 1/32768 on load)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for the start/stop barriers and the max-over-ranks time (nccl = "
+                         "RCCL over xGMI; gloo lets several ranks share one GPU for a rehearsal of the N>1 path)")
     ap.add_argument("--precision", default="fp32", choices=list(PRECISIONS),
                     help="CNN convolutions: fp32 MFMA (config 2, default), bf16 (config 4), or bf16x3 "
                          "(config 2 at fp32-grade accuracy on split-bf16 MFMA); front-end fp32 always")
@@ -128,10 +131,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"# note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and local >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPU(s) visible")
+    local = local % ndev   # (gloo rehearsal: ranks may share a GPU)
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
@@ -175,9 +185,10 @@ def main():
     elapsed = time.perf_counter() - t0
     launch_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
 
-    t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([elapsed, launch_ms], dtype=torch.float64,
+                     device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)   # the slowest rank's time
     elapsed, launch_ms = float(t[0]), float(t[1])
     finite = bool(torch.isfinite(logits).all())
 
@@ -204,7 +215,8 @@ def main():
             "config": {"workload": PRECISIONS[args.precision][1],
                        "audio": "fp32 samples" if args.audio == "f32" else "int16 PCM samples",
                        "batch_per_gpu": B, "global_batch": world * B, "seq_len": 16000,
-                       "parallelism": f"dp{world} (per-rank clip split, no collectives)"},
+                       "parallelism": f"dp{world} (per-rank clip split, no collectives)",
+                       **({"dist_backend": args.dist_backend} if world > 1 else {})},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1),
                          "peak_basis": peak_basis,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4),

@@ -18,10 +18,6 @@ key = sys.argv[1] if len(sys.argv) > 1 else "wk_fused_kernelIfLi0ELb0E"
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-signed-zeros", "-ffp-contract=fast",
        "-fno-slp-vectorize", "-DWK_ASM_MARKS", "-I", f"{R}/include", "-I", f"{R}/esp32-wake-word_amd/csrc",
        *sys.argv[2:], "--cuda-device-only", "-S", f"{R}/esp32-wake-word_amd/csrc/wk_fused.hip", "-o", "/tmp/asm_phases.s"]
-subprocess.run(cmd, check=True, capture_output=True)
-text = open("/tmp/asm_phases.s").read()
-m = [x for x in re.finditer(r"^(_Z\S+):", text, re.M) if key in x.group(1)][0]
-body = text[m.end():text.find(".Lfunc_end", m.end())]
 
 
 def cls(op, line):
@@ -50,21 +46,30 @@ def cls(op, line):
     return "other"
 
 
-segs, cur, label = [], Counter(), "start"
-for ln in body.split("\n"):
-    s = ln.strip()
-    mk = re.search(r";WKMARK (\w+)", s)
-    if mk:
-        segs.append((label + "->" + mk.group(1), cur))
-        cur, label = Counter(), mk.group(1)
-        continue
-    if not s or s.startswith((".", ";", "//")) or s.endswith(":"):
-        continue
-    cur[cls(s.split()[0], s)] += 1
-segs.append((label + "->end", cur))
-cols = ["valu", "valu_pk", "dpp", "cndmask", "trans", "mfma", "lds", "vmem", "salu", "waitcnt", "nop"]
-print(f"{'segment':18s}" + "".join(f"{c:>8s}" for c in cols) + f"{'total':>8s}")
-for name, c in segs:
-    if sum(c.values()) == 0:
-        continue
-    print(f"{name:18s}" + "".join(f"{c[k]:8d}" for k in cols) + f"{sum(c.values()):8d}")
+def main():
+    subprocess.run(cmd, check=True, capture_output=True)
+    text = open("/tmp/asm_phases.s").read()
+    m = [x for x in re.finditer(r"^(_Z\S+):", text, re.M) if key in x.group(1)][0]
+    body = text[m.end():text.find(".Lfunc_end", m.end())]
+    segs, cur, label = [], Counter(), "start"
+    for ln in body.split("\n"):
+        s = ln.strip()
+        mk = re.search(r";WKMARK (\w+)", s)
+        if mk:
+            segs.append((label + "->" + mk.group(1), cur))
+            cur, label = Counter(), mk.group(1)
+            continue
+        if not s or s.startswith((".", ";", "//")) or s.endswith(":"):
+            continue
+        cur[cls(s.split()[0], s)] += 1
+    segs.append((label + "->end", cur))
+    cols = ["valu", "valu_pk", "dpp", "cndmask", "trans", "mfma", "lds", "vmem", "salu", "waitcnt", "nop"]
+    print(f"{'segment':18s}" + "".join(f"{c:>8s}" for c in cols) + f"{'total':>8s}")
+    for name, c in segs:
+        if sum(c.values()) == 0:
+            continue
+        print(f"{name:18s}" + "".join(f"{c[k]:8d}" for k in cols) + f"{sum(c.values()):8d}")
+
+
+if __name__ == "__main__":
+    main()
