@@ -195,6 +195,11 @@ wk_status wk_check_device_errors(wk_handle* h, uint32_t* flags_out) {
   });
 }
 
+// Convolution arithmetic of the fused kernels (wk_fused.hip kConvF32 / kConvBf16 / kConvBf16x3).
+static int conv_mode_of(const wk_handle* h) {
+  return h->cfg.precision == WK_PREC_BF16 ? 1 : (h->cfg.precision == WK_PREC_BF16X3 ? 2 : 0);
+}
+
 static wk_status check_audio(const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len, int64_t clip_stride,
                              bool mode_b) {
   if (batch < 0) return invalid("batch < 0");
@@ -225,14 +230,11 @@ wk_status wk_cnn(wk_handle* h, const float* d_feats, int64_t batch, float* d_log
   if (!h) return invalid("wk_cnn: null handle");
   if (!h->d_weights) return invalid("wk_cnn: handle created without weights");
   if (batch < 0 || (batch > 0 && (!d_feats || !d_logits))) return invalid("wk_cnn: bad arguments");
-  if (h->cfg.precision == WK_PREC_BF16 || h->cfg.precision == WK_PREC_BF16X3) {
-    g_last_error = "wk_cnn: bf16 convolutions run inside the fused kernel only (use wk_forward)";
-    return WK_ERR_UNSUPPORTED;
-  }
   return on_device(h->cfg.device, [&]() -> wk_status {
     hipError_t e = h->cfg.precision == WK_PREC_INT8
                        ? wk::launch_int8_cnn(d_feats, batch, h->d_int8, d_logits, 4 * h->n_cu, (hipStream_t)stream)
-                       : wk::launch_cnn(d_feats, batch, h->d_weights, d_logits, false, h->n_cu, (hipStream_t)stream);
+                       : wk::launch_cnn_fused(d_feats, batch, h->d_packed, h->d_bf16, conv_mode_of(h), d_logits, h->n_cu,
+                                              (hipStream_t)stream);
     return e == hipSuccess ? WK_OK : hip_fail(e, "cnn launch");
   });
 }
@@ -250,10 +252,9 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
   if (batch > 0 && !d_logits) return invalid("wk_forward: null logits");
   const bool int8 = h->cfg.precision == WK_PREC_INT8;
   return on_device(h->cfg.device, [&]() -> wk_status {
-    if ((!h->unfused && !int8) || h->d_bf16) {   // bf16 convolutions exist only in the fused kernel
-      const int conv_mode = h->cfg.precision == WK_PREC_BF16 ? 1 : (h->cfg.precision == WK_PREC_BF16X3 ? 2 : 0);
+    if (!h->unfused && !int8) {
       hipError_t e = wk::launch_fused(dtype == WK_DTYPE_I16, d_audio, batch, clip_stride, h->d_packed, h->d_bf16,
-                                      conv_mode, d_logits, d_feats_or_null, h->n_cu, (hipStream_t)stream, h->d_err,
+                                      conv_mode_of(h), d_logits, d_feats_or_null, h->n_cu, (hipStream_t)stream, h->d_err,
                                       h->fused_exp);
       return e == hipSuccess ? WK_OK : hip_fail(e, "fused launch");
     }
@@ -274,7 +275,8 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
                                          2 * h->n_cu, 0.97f, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(e, "frontend launch");
       e = int8 ? wk::launch_int8_cnn(feats, n, h->d_int8, d_logits + c0, 4 * h->n_cu, (hipStream_t)stream)
-               : wk::launch_cnn(feats, n, h->d_weights, d_logits + c0, false, h->n_cu, (hipStream_t)stream);
+               : wk::launch_cnn_fused(feats, n, h->d_packed, h->d_bf16, conv_mode_of(h), d_logits + c0, h->n_cu,
+                                      (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(e, "cnn launch");
     }
     if (ws_lock.owns_lock()) {

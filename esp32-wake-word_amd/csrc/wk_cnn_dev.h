@@ -1,5 +1,13 @@
-// wk_cnn_dev.h -- device helpers of the xiaoa CNN on fp32 MFMA (shared by
-// wk_cnn.hip and wk_fused.hip).  See wk_cnn.hip for the design notes.
+// wk_cnn_dev.h -- device helpers of the xiaoa CNN (LightweightKWS,
+// ml_models/src/wakeModel.py:4-34) on the matrix cores, used by the CNN role of
+// wk_fused.hip (the fused kernel and the standalone CNN kernel).
+//
+//   conv(13->32,k3,p1) ReLU maxpool2 -> conv(32->64) ReLU pool -> conv(64->128)
+//   ReLU pool -> mean over time -> Linear(128,64) ReLU -> Linear(64,1)
+//
+// Each conv is an implicit GEMM D[co][t] = sum_k W[co][k] X[k][t] over
+// [clip][t][ci] LDS images: fp32 by Winograd F(2,3) on v_mfma_f32_16x16x4_f32,
+// bf16 / split-bf16 directly on bf16 MFMA.
 #pragma once
 #include "wk_common.h"
 
@@ -13,38 +21,6 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ float swap_adjacent(float v) {  // lane l <- lane l^1
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
-}
-
-// Two N-tiles (16 time columns each) of one conv layer, sharing the A fragments.
-// boff = lane part + clip*CLIP + t0; step s covers k = 4s..4s+3 = (tap, ci0..ci0+3).
-// CHUNK > 0 fences the instruction stream every CHUNK steps so the B-fragment
-// LDS reads are not all hoisted ahead of the MFMAs (VGPR budget of the fused
-// kernel); CHUNK = 0 leaves scheduling to the compiler.
-template <int NSTEP, int CIP, int SPT, int CHUNK = 0>
-__device__ __forceinline__ void conv_pair(const float* __restrict__ act, const float (&wf)[NSTEP], int boff_a,
-                                          int boff_b, f32x4& acc_a, f32x4& acc_b) {
-#pragma unroll
-  for (int s = 0; s < NSTEP; ++s) {
-    const int off = (s % SPT) * 4 * CIP + s / SPT;
-    acc_a = mfma4(wf[s], act[boff_a + off], acc_a);
-    acc_b = mfma4(wf[s], act[boff_b + off], acc_b);
-    if (CHUNK > 0 && (s % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-// ReLU -> maxpool(2) -> store the pooled row into the next layer's image.
-template <int CIP_N, int CLIP_N, int TN>
-__device__ __forceinline__ void epi_pool(const f32x4& acc, float* __restrict__ next, int co0, int clip, int t0,
-                                         int lane) {
-  const int t = t0 + (lane & 15);
-  const int tp = t >> 1;
-  const bool w = !(lane & 1) && tp < TN;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float v = fmaxf(acc[r], 0.0f);
-    v = fmaxf(v, swap_adjacent(v));
-    if (w) next[(co0 + 4 * (lane >> 4) + r) * CIP_N + clip * CLIP_N + 1 + tp] = v;
-  }
 }
 
 // ReLU -> maxpool(2) (15 -> 7, floor) -> mean over the 7 pooled steps.
@@ -203,32 +179,6 @@ __device__ __forceinline__ void epi_pool_bf3(const f32x4& acc, uint16_t* __restr
   }
 }
 
-// ---- fp32 convolutions from [clip][t][ci] images (ci-blocked K order) ----
-// MFMA K order is free as long as A and B agree: lane group q = lane >> 4
-// takes ci = 16 cb + 4 q + j at step (tap, cb, j), so the B values of 4
-// consecutive steps are 4 consecutive ci at one (t + tap) row -- one
-// ds_read_b128 per 4 v_mfma_f32_16x16x4f32 (A packed to match,
-// wk_kernels.h pack_fragments).  NSTEP = 3 taps * CB ci-blocks * 4.
-template <int CB, int CIP, int CHUNK = 0>
-__device__ __forceinline__ void conv_pair_v(const float* __restrict__ img, const float (&wf)[12 * CB], int boff_a,
-                                            int boff_b, f32x4& acc_a, f32x4& acc_b) {
-#pragma unroll
-  for (int g = 0; g < 3 * CB; ++g) {   // g = tap * CB + cb
-    const int off = (g / CB) * CIP + 16 * (g % CB);
-    const float4 ba = *reinterpret_cast<const float4*>(img + boff_a + off);
-    const float4 bb = *reinterpret_cast<const float4*>(img + boff_b + off);
-    acc_a = mfma4(wf[4 * g + 0], ba.x, acc_a);
-    acc_b = mfma4(wf[4 * g + 0], bb.x, acc_b);
-    acc_a = mfma4(wf[4 * g + 1], ba.y, acc_a);
-    acc_b = mfma4(wf[4 * g + 1], bb.y, acc_b);
-    acc_a = mfma4(wf[4 * g + 2], ba.z, acc_a);
-    acc_b = mfma4(wf[4 * g + 2], bb.z, acc_b);
-    acc_a = mfma4(wf[4 * g + 3], ba.w, acc_a);
-    acc_b = mfma4(wf[4 * g + 3], bb.w, acc_b);
-    if (CHUNK > 0 && (g % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
 // ---- fp32 convolutions by Winograd F(2,3) (the fp32 path) ---------------
 // conv1d k3 p1 (cross-correlation) for the output pair (2p, 2p+1) from the
 // four input rows d_r = x[2p - 1 + r] (image rows 2p + r):
@@ -304,24 +254,6 @@ __device__ __forceinline__ void epi_wino_gap(const f32x4 (&m)[4], float* __restr
     s += dpp<0x141>(s);
     if (p == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s / 7.0f;
   }
-}
-
-// ReLU -> maxpool(2) -> this lane's 4 pooled channels (consecutive co) as one
-// 16-byte store into the next layer's fp32 [clip][t][ci] image.
-template <int CIP_N, int TP_N, int TN>
-__device__ __forceinline__ void epi_pool_v(const f32x4& acc, float* __restrict__ next, int co0, int clip, int t0,
-                                           int lane) {
-  const int t = t0 + (lane & 15);
-  const int tp = t >> 1;
-  float v[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float x = fmaxf(acc[r], 0.0f);
-    v[r] = fmaxf(x, swap_adjacent(x));
-  }
-  if (!(lane & 1) && tp < TN)
-    *reinterpret_cast<float4*>(next + (clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4)) =
-        make_float4(v[0], v[1], v[2], v[3]);
 }
 
 }  // namespace wk

@@ -390,35 +390,40 @@ __device__ __forceinline__ void dct_cmvn_clip(const float* __restrict__ lbuf, in
 // ---------------------------------------------------------------------------
 // CNN role (waves 8-15): batches of NBF clips from the conv1 image.
 // ---------------------------------------------------------------------------
-// FEATS: the launch also writes the CMVN'd features (parity dumps).  A
-// template flag rather than a null test, so the product kernel carries no
-// feature-store code (its address registers pushed the fp32 build to spill).
-template <int CM, bool FEATS>   // kConvF32 / kConvBf16 / kConvBf16x3
-__device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ pk, const uint16_t* __restrict__ pkb,
-                                         int64_t n_mine, float* __restrict__ logits, float* __restrict__ feats_out,
-                                         int cw, int lane, int exp_flags) {
-  const float* L = smem + kLOff;
-  const float* L1 = smem + kL1Off;
-  float* F0 = smem + kF0Off;
-  float* F1 = smem + kF1Off;
-  float* F2 = smem + kF2Off;
-  uint16_t* B0 = reinterpret_cast<uint16_t*>(smem + kB0Off);
-  uint16_t* B1 = reinterpret_cast<uint16_t*>(smem + kB1Off);
-  uint16_t* B2 = reinterpret_cast<uint16_t*>(smem + kB2Off);
-  uint16_t* X0 = reinterpret_cast<uint16_t*>(smem + kX0Off);
-  uint16_t* X1 = reinterpret_cast<uint16_t*>(smem + kX1Off);
-  uint16_t* X2 = reinterpret_cast<uint16_t*>(smem + kX2Off);
+// Where the CNN role's LDS lives: the fused kernel's carve window
+// [kGOff, kImgEnd) -- pooled features, classifier partials, control words, the
+// conv images -- at `base + offset` (base = smem in the fused kernel; the
+// standalone CNN kernel below places two such windows per workgroup).
+// SRC supplies the conv1 input image of each clip (interface below):
+//   init(cw, lane)   once per wave;
+//   ready(i)         whether clip i's image can be made without waiting;
+//   wait(i)          block until it can;
+//   load(i, slot)    write clip i's normalised [63][13] MFCC into conv1 slot `slot`.
+// The fused kernel's source is the DCT + CMVN of the front-end's log-mel
+// (LogmelSrc); the standalone CNN's is the caller's features in HBM (FeatSrc).
+template <int CM, class SRC>   // kConvF32 / kConvBf16 / kConvBf16x3
+__device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ pk, const uint16_t* __restrict__ pkb,
+                                         int64_t n_mine, int64_t clip_base, int64_t clip_step,
+                                         float* __restrict__ logits, int cw, int lane, SRC& src) {
+  float* F0 = base + kF0Off;
+  float* F1 = base + kF1Off;
+  float* F2 = base + kF2Off;
+  uint16_t* B0 = reinterpret_cast<uint16_t*>(base + kB0Off);
+  uint16_t* B1 = reinterpret_cast<uint16_t*>(base + kB1Off);
+  uint16_t* B2 = reinterpret_cast<uint16_t*>(base + kB2Off);
+  uint16_t* X0 = reinterpret_cast<uint16_t*>(base + kX0Off);
+  uint16_t* X1 = reinterpret_cast<uint16_t*>(base + kX1Off);
+  uint16_t* X2 = reinterpret_cast<uint16_t*>(base + kX2Off);
   constexpr bool BF = CM == kConvBf16, X3 = CM == kConvBf16x3;
   constexpr int kLoW = kNumPackedBf16;   // the xl fragments follow the xh ones (pack_fragments_bf16x3)
   const auto rsb = make_rsrc(pkb, 2 * kNumPackedBf16 * (X3 ? 2 : 1));
   auto frag_bf = [&](int elem_off) -> s8 {   // one lane's 8 bf16 of the fragment at elem_off (x 64 lanes x 8)
     return __builtin_bit_cast(s8, __builtin_amdgcn_raw_buffer_load_b128(rsb, 16 * lane, 2 * elem_off, 0));
   };
-  float* Gp = smem + kGOff;
-  float* FCP = smem + kFcpOff;
-  unsigned* ctrl = reinterpret_cast<unsigned*>(smem + kCtrlOff);
+  float* Gp = base + kGOff;
+  float* FCP = base + kFcpOff;
+  unsigned* ctrl = reinterpret_cast<unsigned*>(base + kCtrlOff);
   const int li = lane & 15, lk = lane >> 4;
-  const int64_t G = gridDim.x;
   unsigned gen = 0;
   const auto rs = make_rsrc(pk, 4 * kNumPacked);
   const int lv = 4 * lane;
@@ -443,31 +448,18 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
   }
   const int64_t n_batches = (n_mine + NBF - 1) / NBF;
-  // Log-mel buffer release (kCtrlLFree + w): wave w < NBF reads only clips
-  // w, w + NBF, w + 2 NBF, ...; its word holds the next clip it will read, so
-  // every clip below it is released.  Waves >= NBF read none.
-  signal_set(ctrl, kCtrlLFree + cw, cw < NBF ? (unsigned)cw : 0xFFFFFFFFu, lane);
+  src.init(cw, lane);
   bool eager_done = false;
-  auto dct_clip = [&](int64_t i, int slot) {
-    float* fo = FEATS ? feats_out + ((int64_t)blockIdx.x + G * i) * (13 * kNFramesB) : nullptr;
-#ifdef WK_DEBUG_LOGMEL
-    dbg_copy_logmel(g_dbg_cnn, i & 1 ? L1 : L, (int64_t)blockIdx.x + G * i, lane);
-#endif
-    dct_cmvn_clip<CM>(i & 1 ? L1 : L, slot, F0, B0, X0, fo, lane);
-    signal_set(ctrl, kCtrlLFree + cw, (unsigned)(i + NBF), lane);
-  };
   // Between the conv phases of batch b (after its conv1 has consumed the conv1
-  // image): if the log-mel of clip 4(b+1) + cw is already there, take its DCT
-  // now, so its buffer goes back to the front-end a whole batch earlier (the
-  // double buffer otherwise stalled the front-end ~13 % of the time in fp32).
+  // image): if clip 4(b+1) + cw's input is already available, make its image
+  // now (fused: its buffer goes back to the front-end a whole batch earlier;
+  // the double buffer otherwise stalled the front-end ~13 % of the time in fp32).
   auto try_eager = [&](int64_t b) {
     if (!WK_DCT_EAGER || cw >= NBF || eager_done) return;
     const int64_t i = (b + 1) * NBF + cw;
     if (i >= n_mine) return;
-    const bool ready = (exp_flags & 2) ||
-                       __builtin_amdgcn_readfirstlane(lds_load(ctrl + kCtrlLReady)) >= 8u * (unsigned)(i + 1);
-    if (ready) {
-      dct_clip(i, cw);
+    if (src.ready(i)) {
+      src.load(i, cw);
       eager_done = true;
     }
   };
@@ -479,8 +471,8 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
     if (cw < NBF && !eager_done) {
       const int64_t i = b * NBF + cw;
       if (i < n_mine) {
-        if (!(exp_flags & 2)) spin_until(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
-        dct_clip(i, cw);
+        src.wait(i);
+        src.load(i, cw);
       }
     }
     eager_done = false;
@@ -665,7 +657,7 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
       acc += __shfl_xor(acc, 16, 64);
       acc += __shfl_xor(acc, 32, 64);
       const int64_t i = b * NBF + cl;
-      if (q == 0 && i < n_mine) logits[(int64_t)blockIdx.x + G * i] = acc;
+      if (q == 0 && i < n_mine) logits[clip_base + clip_step * i] = acc;
     }
     try_eager(b);
     WK_STAMP(8);
@@ -675,6 +667,45 @@ __device__ __forceinline__ void cnn_role(float* smem, const float* __restrict__ 
   }
   WK_STAMP_FLUSH(8 + cw);
 }
+
+// The fused kernel's clip source: DCT-II + CMVN of the front-end's log-mel
+// image (dct_cmvn_clip), with the front-end hand-off protocol.
+// FEATS: the launch also writes the CMVN'd features (parity dumps).  A
+// template flag rather than a null test, so the product kernel carries no
+// feature-store code (its address registers pushed the fp32 build to spill).
+template <int CM, bool FEATS>
+struct LogmelSrc {
+  float* smem;
+  unsigned* ctrl;
+  float* feats_out;
+  int64_t clip_base, clip_step;
+  int cw, lane, exp_flags;
+  // Log-mel buffer release (kCtrlLFree + w): wave w < NBF reads only clips
+  // w, w + NBF, w + 2 NBF, ...; its word holds the next clip it will read, so
+  // every clip below it is released.  Waves >= NBF read none.
+  __device__ __forceinline__ void init(int cw_, int lane_) {
+    cw = cw_;
+    lane = lane_;
+    signal_set(ctrl, kCtrlLFree + cw, cw < NBF ? (unsigned)cw : 0xFFFFFFFFu, lane);
+  }
+  __device__ __forceinline__ bool ready(int64_t i) const {
+    return (exp_flags & 2) ||
+           __builtin_amdgcn_readfirstlane(lds_load(ctrl + kCtrlLReady)) >= 8u * (unsigned)(i + 1);
+  }
+  __device__ __forceinline__ void wait(int64_t i) const {
+    if (!(exp_flags & 2)) spin_until(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
+  }
+  __device__ __forceinline__ void load(int64_t i, int slot) const {
+    float* fo = FEATS ? feats_out + (clip_base + clip_step * i) * (13 * kNFramesB) : nullptr;
+#ifdef WK_DEBUG_LOGMEL
+    dbg_copy_logmel(g_dbg_cnn, smem + (i & 1 ? kL1Off : kLOff), clip_base + clip_step * i, lane);
+#endif
+    dct_cmvn_clip<CM>(smem + (i & 1 ? kL1Off : kLOff), slot, smem + kF0Off,
+                      reinterpret_cast<uint16_t*>(smem + kB0Off), reinterpret_cast<uint16_t*>(smem + kX0Off), fo,
+                      lane);
+    signal_set(ctrl, kCtrlLFree + cw, (unsigned)(i + NBF), lane);
+  }
+};
 
 template <typename T, int CM, bool FEATS>
 __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __restrict__ audio, int64_t batch,
@@ -705,7 +736,11 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
 #endif
   } else {
 #ifndef WK_EXPERIMENT_NO_CNN
-    if (!(exp_flags & 1)) cnn_role<CM, FEATS>(smem, wts, wbf, n_mine, logits, feats_out, wave - 8, lane, exp_flags);
+    if (!(exp_flags & 1)) {
+      LogmelSrc<CM, FEATS> src = {smem, reinterpret_cast<unsigned*>(smem + kCtrlOff), feats_out, (int64_t)blockIdx.x,
+                                  (int64_t)gridDim.x, 0, 0, exp_flags};
+      cnn_role<CM>(smem, wts, wbf, n_mine, (int64_t)blockIdx.x, (int64_t)gridDim.x, logits, wave - 8, lane, src);
+    }
 #endif
   }
   // Protocol health: a spin that timed out set the workgroup's abort word, and
@@ -717,6 +752,78 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
     const unsigned ab = lds_load(reinterpret_cast<unsigned*>(smem + kCtrlOff) + kCtrlAbort);
     if (ab) __hip_atomic_store(err, ab == 1u ? 1u : 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Standalone CNN (wk_cnn: LightweightKWS.forward on caller features, the ONNX
+// `run` surface).  The same CNN role as the fused kernel, fed from HBM: each
+// 1024-thread workgroup runs TWO independent CNN roles of 8 waves, each with its
+// own carve of images / pooled features / control words, on interleaved clips.
+// FeatSrc copies clip i's CMVN'd features [13][63] (wakeModel.py input layout)
+// into the conv1 image as [t][ci] rows: lane t reads its frame's 13
+// coefficients (63 lanes of one coefficient are one coalesced 252-byte read).
+// ---------------------------------------------------------------------------
+template <int CM>
+struct FeatSrc {
+  const float* feats;
+  float* base;   // the role's carve base (cnn_role's `base`)
+  int64_t clip_base, clip_step;
+  int lane;
+  __device__ __forceinline__ void init(int, int lane_) { lane = lane_; }
+  __device__ __forceinline__ bool ready(int64_t) const { return true; }
+  __device__ __forceinline__ void wait(int64_t) const {}
+  __device__ __forceinline__ void load(int64_t i, int slot) const {
+    const float* f = feats + (clip_base + clip_step * i) * (13 * kNFramesB);
+    if (lane >= kNFramesB) return;
+    float y[13];
+#pragma unroll
+    for (int c = 0; c < 13; ++c) y[c] = __builtin_nontemporal_load(f + c * kNFramesB + lane);
+    const int row = slot * I0_TP + 1 + lane;
+    if constexpr (CM == kConvBf16) {
+      uint16_t* B0 = reinterpret_cast<uint16_t*>(base + kB0Off) + row * I0_CIP;
+#pragma unroll
+      for (int c = 0; c < 12; c += 4)
+        *reinterpret_cast<uint2*>(B0 + c) = make_uint2(bf16_bits(y[c]) | (bf16_bits(y[c + 1]) << 16),
+                                                       bf16_bits(y[c + 2]) | (bf16_bits(y[c + 3]) << 16));
+      B0[12] = (uint16_t)bf16_bits(y[12]);
+    } else if constexpr (CM == kConvBf16x3) {
+      uint16_t* X0 = reinterpret_cast<uint16_t*>(base + kX0Off) + row * X0_CIP;
+#pragma unroll
+      for (int c = 0; c < 13; ++c) {
+        const uint32_t h = bf16_bits(y[c]);
+        X0[c] = (uint16_t)h;
+        X0[16 + c] = (uint16_t)bf16_bits(y[c] - __uint_as_float(h << 16));
+      }
+    } else {
+      float* F0 = base + kF0Off + row * F0_CIP;
+#pragma unroll
+      for (int c = 0; c < 12; c += 4) *reinterpret_cast<f32x4*>(F0 + c) = f32x4{y[c], y[c + 1], y[c + 2], y[c + 3]};
+      F0[12] = y[12];
+    }
+  }
+};
+
+constexpr int kCnnCarve = kImgEnd - kGOff;   // floats per CNN role: the fused carve window [kGOff, kImgEnd)
+constexpr int kCnnLds = 2 * kCnnCarve;
+static_assert(kCnnLds * 4 <= 163840, "standalone CNN LDS budget");
+static_assert(kCnnCarve % 4 == 0 && kGOff % 4 == 0, "16-byte aligned carves");
+
+template <int CM>
+__global__ __launch_bounds__(kFusedBlock, 4) void wk_cnn_fused_kernel(const float* __restrict__ feats, int64_t batch,
+                                                                     const float* __restrict__ wts,
+                                                                     const uint16_t* __restrict__ wbf,
+                                                                     float* __restrict__ logits) {
+  __shared__ __attribute__((aligned(16))) float smem[kCnnLds];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < kCnnLds; i += kFusedBlock) smem[i] = 0.0f;   // guards, padding ci, control words
+  __syncthreads();
+  const int role = wave >> 3;
+  float* base = smem + role * kCnnCarve - kGOff;   // base + kGOff = this role's window
+  const int64_t cb = 2 * (int64_t)blockIdx.x + role, cs = 2 * (int64_t)gridDim.x;
+  const int64_t n_mine = batch > cb ? (batch - 1 - cb) / cs + 1 : 0;
+  FeatSrc<CM> src = {feats, base, cb, cs, 0};
+  cnn_role<CM>(base, wts, wbf, n_mine, cb, cs, logits, wave & 7, lane, src);
 }
 
 }  // namespace
@@ -768,6 +875,24 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
     else WK_FUSED_LAUNCH(float, kConvF32);
   }
 #undef WK_FUSED_LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t launch_cnn_fused(const float* feats, int64_t batch, const float* w, const uint16_t* wbf, int conv_mode,
+                            float* logits, int grid_cap, hipStream_t stream) {
+  if (batch == 0) return hipSuccess;
+  if (conv_mode != kConvF32 && !wbf) return hipErrorInvalidValue;
+  const int64_t roles = (batch + NBF - 1) / NBF;   // at least one batch of clips per CNN role
+  const int grid = (int)((roles + 1) / 2 < grid_cap ? (roles + 1) / 2 : grid_cap);
+  if (conv_mode == kConvBf16)
+    hipLaunchKernelGGL(wk_cnn_fused_kernel<kConvBf16>, dim3(grid), dim3(kFusedBlock), 0, stream, feats, batch, w, wbf,
+                       logits);
+  else if (conv_mode == kConvBf16x3)
+    hipLaunchKernelGGL(wk_cnn_fused_kernel<kConvBf16x3>, dim3(grid), dim3(kFusedBlock), 0, stream, feats, batch, w,
+                       wbf, logits);
+  else
+    hipLaunchKernelGGL(wk_cnn_fused_kernel<kConvF32>, dim3(grid), dim3(kFusedBlock), 0, stream, feats, batch, w, wbf,
+                       logits);
   return hipGetLastError();
 }
 

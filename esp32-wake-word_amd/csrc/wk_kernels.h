@@ -35,11 +35,6 @@ hipError_t launch_frontend(bool mode_b, bool i16, const void* audio, int64_t bat
                            int64_t clip_stride, float* out, int esp_pack, int cmvn, int grid_cap,
                            float pre_emphasis, hipStream_t stream);   // pre_emphasis: 0.97 (mfcc.c:445), 0 = none
 
-// CNN (wk_cnn.hip): feats [B][13][63] -> logits [B].  `w` = device weight
-// blob in the packed WK_NUM_WEIGHTS layout of include/wakeword.h.
-hipError_t launch_cnn(const float* feats, int64_t batch, const float* w, float* logits, bool bf16,
-                      int grid_cap, hipStream_t stream);
-
 // Fused front-end + CNN (wk_fused.hip), mode B only.
 // w = fp32 fragment-major weights (pack_fragments); wbf = bf16 conv fragments
 // (pack_fragments_bf16; hi then lo parts for split bf16) for conv_mode 1
@@ -49,6 +44,11 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
                         unsigned* err,        // host-visible protocol error word (see wk_fused_kernel), may be null
                         int exp_flags = 0);   // timing experiments (-DWK_DEBUG_EXPERIMENTS builds only): 1 = FE role
                                               // only, 2 = CNN role only; wrong logits
+
+// CNN on caller features (wk_fused.hip, the fused kernel's CNN role fed from
+// HBM): feats [B][13][63] -> logits [B]; conv_mode as launch_fused.
+hipError_t launch_cnn_fused(const float* feats, int64_t batch, const float* w, const uint16_t* wbf, int conv_mode,
+                            float* logits, int grid_cap, hipStream_t stream);
 
 // int8 CNN in the device's esp-dl arithmetic (wk_int8.hip); feats [B][13][63] fp32.
 constexpr int kNumInt8Weights = 3 * 13 * 32 + 3 * 32 * 64 + 3 * 64 * 128 + 128 * 64 + 64;

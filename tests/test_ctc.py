@@ -140,3 +140,25 @@ def test_ctc_fp16_ragged_vocab(vocab):
     top2 = torch.topk(ref_lp, 2, dim=-1).values
     ok = (top2[..., 0] - top2[..., 1]) > 0.2
     assert (lp.argmax(-1) == ref_lp.argmax(-1))[ok].all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_ctc_bit_repeatable_at_scale(precision):
+    """Several hundred utterances through features + BiGRU + output layer,
+    three times: tokens, lengths and log-probs bit-identical run to run (the
+    persistent recurrence and the fused output kernel carry no timing
+    dependence)."""
+    import wakeword
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    m = CO.make_model(V, seed=3)
+    g = wakeword.CTCModel(CO.flat_weights(m), V, precision=precision)
+    audio = wakeword.synth_clips(77, 0, 384, 48000)
+    ref = None
+    for _ in range(3):
+        out = [t.clone() for t in g.decode(g.features(audio, n_samples=48000), return_log_probs=True)]
+        if ref is None:
+            ref = out
+        else:
+            assert all(torch.equal(a, b) for a, b in zip(ref, out))

@@ -38,10 +38,20 @@ def test_bf16_synth_vs_oracle_and_batch_invariance(m16, xiaoa_sd, n):
     np.testing.assert_array_equal(one, got[:1])      # per-clip results do not depend on the batch
 
 
-def test_bf16_cnn_only_entry_is_refused(m16):
+@pytest.mark.parametrize("prec,atol", [("bf16", BF16_LOGIT_ATOL), ("bf16x3", 1e-3)])
+def test_cnn_only_entry_all_precisions(gpu, golden_dir, xiaoa_sd, prec, atol):
+    """wk_cnn (LightweightKWS.forward on given features) runs the fused
+    kernel's CNN role fed from HBM in every precision: the reference module's
+    golden logits on the golden features, and the fused path's logits for the
+    same clips (ragged batch: 37 clips, two CNN roles per workgroup)."""
     import wakeword
-    with pytest.raises(wakeword.WakewordError, match="UNSUPPORTED"):
-        m16(np.zeros((2, 13, 63), np.float32))
+    m = wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"), precision=prec)
+    g = np.load(os.path.join(golden_dir, "synth.npz"))
+    got = m(g["feats"]).reshape(-1).cpu().numpy()
+    assert np.abs(got - g["logits"].reshape(-1)).max() <= atol
+    x = O.synth_clips(51, 0, 37, 16000)
+    logit_fused, feats = m.detect(x, return_features=True)
+    np.testing.assert_allclose(m(feats).reshape(-1).cpu().numpy(), logit_fused.cpu().numpy(), atol=1e-5)
 
 
 # ---- WK_PREC_BF16X3: split-bf16 convolutions held to the fp32 logit tolerance.
