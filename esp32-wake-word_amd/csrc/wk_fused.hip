@@ -217,28 +217,34 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   // w + 8r + 16(g&1) + 32(g>>1) (groups 0/1 16 frames apart: disjoint LDS
   // banks).  A dynamic hand-out through an LDS counter was measured slower:
   // the atomic's return latency lands on the prefetch path.
-  auto clip_of = [&](int64_t i) { return (int64_t)blockIdx.x + G * i; };
-  auto prefetch = [&](int64_t i, int r, Raw<T>& dst) {
-    if (i < n_mine) {
-      const int fl = fw + 8 * r + slot_base;
-      const bool general = kEdge && ((r == 0 && fw == 0) || (r == 1 && fw == 6));   // frame 0 / frame 62
-      load_raw<true>(make_rsrc(audio + clip_of(i) * clip_stride, kWinSamples * sizeof(T)), 256 * fl - 160, j,
-                     kWinSamples, fl < kNFramesB, general, dst);
-    }
+  //
+  // Prefetch context of a round, built once per round: the clip's buffer
+  // resource and whether the round holds a reflected edge frame (frame 0 in
+  // wave 0 round 0, frame 62 in wave 6 round 1; wave-uniform).  Past the
+  // workgroup's last clip the resource has num_records 0, so those loads
+  // return 0 without a branch; the padding slot (frame 63) needs no lane mask
+  // either, since its samples past the clip's end come back 0 from the same
+  // bounds check.  (Rebuilt inside each of the four prefetch parts, the 64-bit
+  // clip address, the `i < n_mine` test and the per-lane `frame < 63` exec mask
+  // cost ~28 scalar/branch instructions per part, ~13 % of a round's issue.)
+  const int64_t step = G * clip_stride;
+  const T* cptr = audio + (int64_t)blockIdx.x * clip_stride;   // clip i of this workgroup
+  constexpr uint32_t kClipBytes = kWinSamples * sizeof(T);
+  struct PfCtx {
+    __amdgpu_buffer_rsrc_t rs;
+    int base;       // first sample of the lane group's frame (before reflection)
+    bool general;   // edge frame: per-lane reflected indices, issued whole with part 0
   };
-
-  // Part k of the prefetch (fe_rest calls it at four points of the round).
-  auto prefetch_part = [&](int64_t i, int r, Raw<T>& dst, int k) {
-    if (i < n_mine) {
-      const int fl = fw + 8 * r + slot_base;
-      const bool general = kEdge && ((r == 0 && fw == 0) || (r == 1 && fw == 6));   // frame 0 / frame 62
-      load_raw_part<true>(make_rsrc(audio + clip_of(i) * clip_stride, kWinSamples * sizeof(T)), 256 * fl - 160, j,
-                          kWinSamples, fl < kNFramesB, general, dst, k);
-    }
+  auto pf_ctx = [&](const T* p, bool ok, int r) -> PfCtx {
+    const int fl = fw + 8 * r + slot_base;
+    return {make_rsrc(p, ok ? kClipBytes : 0u), 256 * fl - 160, kEdge && ((r == 0 && fw == 0) || (r == 1 && fw == 6))};
   };
 
   Raw<T> pf;
-  prefetch(0, 0, pf);
+  {
+    const PfCtx c0 = pf_ctx(cptr, n_mine > 0, 0);
+    load_raw<true>(c0.rs, c0.base, j, kWinSamples, true, c0.general, pf);
+  }
   WK_STAMP_INIT
   for (int64_t i = 0; i < n_mine; ++i) {
 #pragma unroll 1
@@ -259,9 +265,9 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       // the prefetch parts issued from inside fe_rest load for all lanes.
       fe_stage0<true>(pf, 256 * fl - 160, kWinSamples, j, general, tb, a);
       WK_STAMP(0);
-      const int64_t ni = r == 0 ? i : i + 1;
-      const int nr = r ^ 1;
-      auto pf_part = [&](int k) { prefetch_part(ni, nr, pf, k); };
+      // next round: (i, 1) after round 0, (i + 1, 0) after round 1
+      const PfCtx nx = r == 0 ? pf_ctx(cptr, true, 1) : pf_ctx(cptr + step, i + 1 < n_mine, 0);
+      auto pf_part = [&](int k) { load_raw_part<true>(nx.rs, nx.base, j, kWinSamples, true, nx.general, pf, k); };
       WK_STAMP(1);
       if (r == 0) {
 #ifndef WK_ABL_NOFEBAR   // timing ablation (tools/debug): no front-end barriers (wrong results)
@@ -269,7 +275,7 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
 #endif
         WK_STAMP(9);
 #ifdef WK_DEBUG_LOGMEL
-        if (wave == 0 && i >= 1) dbg_copy_logmel(g_dbg_fe, (i - 1) & 1 ? L1 : L, clip_of(i - 1), lane);
+        if (wave == 0 && i >= 1) dbg_copy_logmel(g_dbg_fe, (i - 1) & 1 ? L1 : L, (int64_t)blockIdx.x + G * (i - 1), lane);
 #endif
       }
       float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
@@ -292,6 +298,7 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
     gen += 8;
     signal_add(ctrl, kCtrlFeBar, lane);
     p_wait = gen;
+    cptr += step;
   }
   WK_STAMP_FLUSH(wave);
 }
@@ -715,6 +722,9 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
                                                                  float* __restrict__ feats_out, unsigned* err,
                                                                  int exp_flags) {
   __shared__ __attribute__((aligned(16))) float smem[kFusedLds];
+#ifndef WK_DEBUG_EXPERIMENTS
+  exp_flags = 0;   // the product kernel folds every experiment branch away (~20 scalar instructions per round)
+#endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
