@@ -179,6 +179,9 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
     y0[n1] = __builtin_fmaf(pre, xm, x0);   // pre = -0.97 (0 for mfcc.c's single-frame variant)
     y1[n1] = __builtin_fmaf(pre, x0, x1);
   }
+  // The windowed pairs are formed in each branch, so the two paths merge on
+  // a[] (register pairs) rather than on y0/y1 (merging the halves cost ~15
+  // v_mov per round to re-pair them on the common path).
   if (MODE_B && general) {   // wave-uniform: the two reflected edge frames only
 #pragma unroll
     for (int n1 = 0; n1 < 10; ++n1) {
@@ -190,12 +193,14 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
       const float xn = j != 15 ? nx : (n1 < 9 ? nx1 : to_f(raw.xb));
       const bool reflected = i0 < 0 || i0 > n - 1;
       const float r0 = __builtin_fmaf(pre, x1, x0), r1 = __builtin_fmaf(pre, xn, x1);
-      y0[n1] = reflected ? r0 : (i0 == 0 ? x0 : y0[n1]);
-      y1[n1] = reflected ? r1 : y1[n1];
+      const float g0 = reflected ? r0 : (i0 == 0 ? x0 : y0[n1]);
+      const float g1 = reflected ? r1 : y1[n1];
+      a[n1] = f2{g0, g1} * w[n1];
     }
-  }
+  } else {
 #pragma unroll
-  for (int n1 = 0; n1 < 10; ++n1) a[n1] = f2{y0[n1], y1[n1]} * w[n1];
+    for (int n1 = 0; n1 < 10; ++n1) a[n1] = f2{y0[n1], y1[n1]} * w[n1];
+  }
 #pragma unroll
   for (int n1 = 10; n1 < 16; ++n1) a[n1] = f2{0.0f, 0.0f};
 }
@@ -241,15 +246,21 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
   for (int n2 = 0; n2 < 16; ++n2) c[n2] = b[n2];
 #else
   const int kc = fe_kcol(j);   // the column this lane transforms in the second pass
+  // The reads are single-dword (volatile: not merged into ds_read2_b32, whose
+  // two consecutive destination registers hold two elements' re parts and
+  // cost ~24 v_mov per round to re-pair as {re, im}); each lands in its half
+  // of c[n2] directly.
+  typedef const volatile __attribute__((address_space(3))) float lds_cvf;
+  lds_cvf* vrow = (lds_cvf*)(row + 17 * kc);
   wave_lds_sync();
 #pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) c[n2].x = row[17 * kc + n2];
+  for (int n2 = 0; n2 < 16; ++n2) c[n2].x = vrow[n2];
   wave_lds_sync();
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) row[17 * k1 + j] = b[k1].y;
   wave_lds_sync();
 #pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) c[n2].y = row[17 * kc + n2];
+  for (int n2 = 0; n2 < 16; ++n2) c[n2].y = vrow[n2];
   wave_lds_sync();
 #endif
   WK_FE_HIT(4);
@@ -320,11 +331,16 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
 #ifdef WK_SPLIT_BPERMUTE
         const float pr = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sv.x)));
         const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sv.y)));
-#else
-        const float pr = dpp<0x121>(dpp<0x140>(sv.x));
-        const float pi = dpp<0x121>(dpp<0x140>(sv.y));
-#endif
         zq = j == 0 ? own : f2{pr, pi};
+#else
+        // row_mirror (lane j <- 15 - j), then row_shr:1 (lane j <- j - 1) with
+        // bound_ctrl off: lane 0 has no source and keeps `old` = its own
+        // partner register -- no lane select.
+        zq.x = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.x), __float_as_int(dpp<0x140>(sv.x)),
+                                                          0x111, 0xF, 0xF, false));
+        zq.y = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), __float_as_int(dpp<0x140>(sv.y)),
+                                                          0x111, 0xF, 0xF, false));
+#endif
 #endif
       } else {
         zq = c[dft16_out(8)];

@@ -122,6 +122,7 @@ static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 // clip per 65k (seen with split-bf16 timing).  The other counters are sound as
 // sums: their producers pass a barrier between consecutive signals.
 enum { kCtrlFeBar = 0, kCtrlCnnBar = 1, kCtrlLReady = 2, kCtrlLFree = 4, kCtrlAbort = 15 };
+static_assert(kCtrlOff % 4 == 0 && kCtrlLFree % 4 == 0, "spin_until_all8 reads the eight LFree words as two uint4");
 // Every spin is bounded (~4M sleeps, well under a second): a protocol bug
 // yields wrong logits and a drained grid, never a hung GPU.
 constexpr unsigned kSpinLimit = 1u << 22;
@@ -131,11 +132,13 @@ __device__ __forceinline__ unsigned lds_load(const unsigned* p) {
 }
 
 // Spin until ctrl[idx] >= v.  On a timeout the workgroup's abort word is set
-// and every later spin returns at once.
+// and every later spin returns at once.  Every iteration is issue time taken
+// from the other waves of the SIMD, so the abort word is polled only every
+// 32nd iteration.
 __device__ __forceinline__ void spin_until(unsigned* ctrl, int idx, unsigned v) {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   for (unsigned n = 0; lds_load(ctrl + idx) < v; ++n) {
-    if (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort)) {
+    if ((n & 31) == 31 && (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort))) {
       __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       break;
     }
@@ -157,14 +160,17 @@ __device__ __forceinline__ void role_sync(unsigned* ctrl, int idx, unsigned& gen
 }
 
 // Spin until ctrl[idx + w] >= v for all w < 8 (same abort rules as spin_until).
+// The eight words are 16-byte aligned (idx = kCtrlLFree = 4): two 16-byte LDS
+// reads per poll instead of eight.
 __device__ __forceinline__ void spin_until_all8(unsigned* ctrl, int idx, unsigned v) {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  const uint4* q = reinterpret_cast<const uint4*>(ctrl + idx);
   for (unsigned n = 0;; ++n) {
-    unsigned m = lds_load(ctrl + idx);
-#pragma unroll
-    for (int w = 1; w < 8; ++w) m = min(m, lds_load(ctrl + idx + w));
+    asm volatile("" ::: "memory");
+    const uint4 a = q[0], b = q[1];
+    const unsigned m = min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w)));
     if (m >= v) break;
-    if (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort)) {
+    if ((n & 31) == 31 && (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort))) {
       __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       break;
     }
