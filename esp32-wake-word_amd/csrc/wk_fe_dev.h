@@ -207,7 +207,8 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
 
 // Stages 1..4 of one frame -> its power row (bins 0..256) in LDS.  All
 // complex arithmetic is packed fp32 (see f2 in wk_common.h).
-// pf(k), k = 0..3, is called at four points of the round (prefetch parts).
+// pf(k), k = 0..3, is called at four points of the round (prefetch parts);
+// pf(-1) just before the round's first write into `row`.
 // TWS: the split's twiddle W512^k, k = kc + 16 k2, is one table value per
 // (lane, k2) (tb.tws) instead of W512^kc x the constant W32^k2 -- one complex
 // multiply instead of two; bin 128 comes from |Z[128]|^2 directly.
@@ -224,6 +225,7 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
   // (twiddles are applied in groups of 4 so their LDS reads do not all
   // sit in VGPRs at once; re parts go straight to the transpose image.)
   f2 b[16];
+  pf(-1);   // the first write into this frame's LDS row follows (fused kernel: wait until the row is free)
   b[0] = a[0];
   row[j] = b[0].x;
 #pragma unroll

@@ -131,18 +131,32 @@ __device__ __forceinline__ unsigned lds_load(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+#ifndef WK_PRIO_FE
+#define WK_PRIO_FE 3      // issue priority of the front-end waves (the critical path; see the kernel)
+#endif
+#ifndef WK_SPIN_SLEEP
+#define WK_SPIN_SLEEP 2   // s_sleep argument (x64 cycles) between polls (2 measured >= 1)
+#endif
+
 // Spin until ctrl[idx] >= v.  On a timeout the workgroup's abort word is set
-// and every later spin returns at once.  Every iteration is issue time taken
-// from the other waves of the SIMD, so the abort word is polled only every
-// 32nd iteration.
+// and every later spin returns at once.  Every poll is issue time taken from
+// the other waves of the SIMD, so a waiting wave drops to issue priority 0
+// (PRIO = the role's priority, restored on exit) and polls the abort word only
+// every 32nd iteration.
+template <int PRIO>
 __device__ __forceinline__ void spin_until(unsigned* ctrl, int idx, unsigned v) {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  for (unsigned n = 0; lds_load(ctrl + idx) < v; ++n) {
-    if ((n & 31) == 31 && (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort))) {
-      __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      break;
+  if (lds_load(ctrl + idx) < v) {
+    if (PRIO > 0) __builtin_amdgcn_s_setprio(0);
+    for (unsigned n = 0;; ++n) {
+      __builtin_amdgcn_s_sleep(WK_SPIN_SLEEP);
+      if (lds_load(ctrl + idx) >= v) break;
+      if ((n & 31) == 31 && (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort))) {
+        __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
     }
-    __builtin_amdgcn_s_sleep(1);
+    if (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
   }
   asm volatile("" ::: "memory");
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -151,30 +165,38 @@ __device__ __forceinline__ void spin_until(unsigned* ctrl, int idx, unsigned v) 
 // Barrier among the 8 waves of one role (LDS counter; s_barrier would also
 // stop the other role's waves).  LDS operations of a wave complete in order,
 // so a wave's data writes are visible before its arrival is.
+template <int PRIO>
 __device__ __forceinline__ void role_sync(unsigned* ctrl, int idx, unsigned& gen, int lane) {
   gen += 8;
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(ctrl + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  spin_until(ctrl, idx, gen);
+  spin_until<PRIO>(ctrl, idx, gen);
 }
 
-// Spin until ctrl[idx + w] >= v for all w < 8 (same abort rules as spin_until).
+// Spin until ctrl[idx + w] >= v for all w < 8 (same rules as spin_until).
 // The eight words are 16-byte aligned (idx = kCtrlLFree = 4): two 16-byte LDS
 // reads per poll instead of eight.
+__device__ __forceinline__ unsigned min8(const unsigned* ctrl, int idx) {
+  asm volatile("" ::: "memory");
+  const uint4* q = reinterpret_cast<const uint4*>(ctrl + idx);
+  const uint4 a = q[0], b = q[1];
+  return min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w)));
+}
+template <int PRIO>
 __device__ __forceinline__ void spin_until_all8(unsigned* ctrl, int idx, unsigned v) {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  const uint4* q = reinterpret_cast<const uint4*>(ctrl + idx);
-  for (unsigned n = 0;; ++n) {
-    asm volatile("" ::: "memory");
-    const uint4 a = q[0], b = q[1];
-    const unsigned m = min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w)));
-    if (m >= v) break;
-    if ((n & 31) == 31 && (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort))) {
-      __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      break;
+  if (min8(ctrl, idx) < v) {
+    if (PRIO > 0) __builtin_amdgcn_s_setprio(0);
+    for (unsigned n = 0;; ++n) {
+      __builtin_amdgcn_s_sleep(WK_SPIN_SLEEP);
+      if (min8(ctrl, idx) >= v) break;
+      if ((n & 31) == 31 && (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort))) {
+        __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
     }
-    __builtin_amdgcn_s_sleep(1);
+    if (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
   }
   asm volatile("" ::: "memory");
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -273,26 +295,33 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       WK_STAMP(0);
       // next round: (i, 1) after round 0, (i + 1, 0) after round 1
       const PfCtx nx = r == 0 ? pf_ctx(cptr, true, 1) : pf_ctx(cptr + step, i + 1 < n_mine, 0);
-      auto pf_part = [&](int k) { load_raw_part<true>(nx.rs, nx.base, j, kWinSamples, true, nx.general, pf, k); };
-      WK_STAMP(1);
-      if (r == 0) {
+      // k = -1: the round is about to write its first power-row element.  In
+      // round 0 that needs every wave done reading clip i-1's rows (its mel);
+      // waiting there rather than before the round lets stage 0, the loads and
+      // the first DFT16 overlap the slower waves' mel.
+      auto pf_part = [&](int k) {
+        if (k >= 0) {
+          load_raw_part<true>(nx.rs, nx.base, j, kWinSamples, true, nx.general, pf, k);
+        } else if (r == 0) {
 #ifndef WK_ABL_NOFEBAR   // timing ablation (tools/debug): no front-end barriers (wrong results)
-        spin_until(ctrl, kCtrlFeBar, p_wait);   // every wave done reading clip i-1's power rows
+          spin_until<WK_PRIO_FE>(ctrl, kCtrlFeBar, p_wait);
 #endif
-        WK_STAMP(9);
+          WK_STAMP(9);
 #ifdef WK_DEBUG_LOGMEL
-        if (wave == 0 && i >= 1) dbg_copy_logmel(g_dbg_fe, (i - 1) & 1 ? L1 : L, (int64_t)blockIdx.x + G * (i - 1), lane);
+          if (wave == 0 && i >= 1) dbg_copy_logmel(g_dbg_fe, (i - 1) & 1 ? L1 : L, (int64_t)blockIdx.x + G * (i - 1), lane);
 #endif
-      }
+        }
+      };
+      WK_STAMP(1);
       float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
       fe_rest<true, decltype(pf_part), (bool)WK_FE_TWS>(a, j, lane, row, tb, w512, 0, pf_part WK_SP_ARG);
     }
     if (exp_flags & 4) __builtin_amdgcn_s_setprio(1); else if (exp_flags & 8) __builtin_amdgcn_s_setprio(0);
 #ifndef WK_ABL_NOFEBAR
-    role_sync(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
+    role_sync<WK_PRIO_FE>(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
 #endif
     WK_STAMP(7);
-    if (i >= 2 && !(exp_flags & 1)) spin_until_all8(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
+    if (i >= 2 && !(exp_flags & 1)) spin_until_all8<WK_PRIO_FE>(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
     WK_STAMP(10);
 #ifndef WK_ABL_NOMEL
     mel_dispatch<true>(wave, P + min(lane, kNFramesB - 1) * kPRow, (i & 1 ? L1 : L) + lane);
@@ -505,7 +534,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       for (int s = 0; s < 12; ++s) w1[s] = buf_load(rs, lv, 4 * (kPkW1 + ((cw & 1) * 12 + s) * 64));
     }
     WK_STAMP(0);
-    role_sync(ctrl, kCtrlCnnBar, gen, lane);   // conv1 image complete
+    role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);   // conv1 image complete
 
     // conv1: co tile (cw&1), clip (cw>>1), 4 t-tiles.
     {
@@ -533,7 +562,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       }
     }
     WK_STAMP(1);
-    role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);
     try_eager(b);
     WK_STAMP(2);
 
@@ -586,7 +615,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
     }
     WK_STAMP(3);
-    role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);
     if (!kW3Batch) try_eager(b);   // (w3 is live from here to the end of conv3)
     WK_STAMP(4);
 
@@ -629,7 +658,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       for (int s = 0; s < 16; ++s) wf1[s] = buf_load(rs, lv, 4 * (kPkF1 + ((cw & 3) * 32 + 16 * (cw >> 2) + s) * 64));
     }
     WK_STAMP(5);
-    role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);
     try_eager(b);
     WK_STAMP(6);
 
@@ -647,7 +676,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
         for (int r = 0; r < 4; ++r) FCP[kh * 64 * NBF + (16 * (cw & 3) + 4 * lk + r) * NBF + li] = acc[r];
       }
     }
-    role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);
     WK_STAMP(7);
 
     // ReLU -> classifier.2 (64 -> 1): lane = (o group q = lane>>2, clip = lane&3).
@@ -675,7 +704,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
     try_eager(b);
     WK_STAMP(8);
 #ifdef WK_SYNC_AFTER_FC2
-    role_sync(ctrl, kCtrlCnnBar, gen, lane);
+    role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);
 #endif
   }
   WK_STAMP_FLUSH(8 + cw);
@@ -706,7 +735,7 @@ struct LogmelSrc {
            __builtin_amdgcn_readfirstlane(lds_load(ctrl + kCtrlLReady)) >= 8u * (unsigned)(i + 1);
   }
   __device__ __forceinline__ void wait(int64_t i) const {
-    if (!(exp_flags & 2)) spin_until(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
+    if (!(exp_flags & 2)) spin_until<0>(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
   }
   __device__ __forceinline__ void load(int64_t i, int slot) const {
     float* fo = FEATS ? feats_out + (clip_base + clip_step * i) * (13 * kNFramesB) : nullptr;
@@ -742,9 +771,6 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
   // The front-end role is the critical path: static issue priority over the
   // CNN role measured +0.5-0.9 % (priority 1-3); the reverse (CNN over
   // front-end) measured -13 %.
-#ifndef WK_PRIO_FE
-#define WK_PRIO_FE 3
-#endif
   if (WK_PRIO_FE > 0 && wave < 8) __builtin_amdgcn_s_setprio(WK_PRIO_FE);
   if (wave < 8) {
 #ifndef WK_EXPERIMENT_NO_FE
