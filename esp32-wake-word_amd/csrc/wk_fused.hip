@@ -505,6 +505,31 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       eager_done = true;
     }
   };
+  // ReLU -> classifier.2 (64 -> 1) of batch bb from the classifier.0 partials:
+  // lane = (o group q = lane>>2, clip = lane&3).  Run by one wave, deferred to
+  // just after the next batch's first barrier (one barrier per batch fewer).
+#ifndef WK_FC2_WAVE
+#define WK_FC2_WAVE 0
+#endif
+  auto fc2 = [&](int64_t bb) {
+    if (cw != WK_FC2_WAVE) return;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int cl = ln & (NBF - 1), q = ln >> 2;
+    float acc = 0.0f;
+#pragma unroll
+    for (int i2 = 0; i2 < 4; ++i2) {
+      const int o = 4 * q + i2;
+      const float h = fmaxf(FCP[o * NBF + cl] + FCP[64 * NBF + o * NBF + cl], 0.0f);
+      acc = __builtin_fmaf(buf_load(rs, 16 * q, 4 * (kPkF2 + i2)), h, acc);
+    }
+    acc += __shfl_xor(acc, 4, 64);
+    acc += __shfl_xor(acc, 8, 64);
+    acc += __shfl_xor(acc, 16, 64);
+    acc += __shfl_xor(acc, 32, 64);
+    const int64_t i = bb * NBF + cl;
+    if (q == 0 && i < n_mine) logits[clip_base + clip_step * i] = acc;
+  };
   WK_STAMP_INIT
   for (int64_t b = 0; b < n_batches; ++b) {
     // DCT-II + CMVN (extract_mfcc.py:70-80): CNN wave s < NBF takes clip
@@ -534,7 +559,8 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       for (int s = 0; s < 12; ++s) w1[s] = buf_load(rs, lv, 4 * (kPkW1 + ((cw & 1) * 12 + s) * 64));
     }
     WK_STAMP(0);
-    role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);   // conv1 image complete
+    role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);   // conv1 image complete (and the previous batch's partials)
+    if (b > 0) fc2(b - 1);
 
     // conv1: co tile (cw&1), clip (cw>>1), 4 t-tiles.
     {
@@ -676,36 +702,15 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
         for (int r = 0; r < 4; ++r) FCP[kh * 64 * NBF + (16 * (cw & 3) + 4 * lk + r) * NBF + li] = acc[r];
       }
     }
-    role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);
-    WK_STAMP(7);
-
-    // ReLU -> classifier.2 (64 -> 1): lane = (o group q = lane>>2, clip = lane&3).
-#ifndef WK_FC2_WAVE
-#define WK_FC2_WAVE 0
-#endif
-    if (cw == WK_FC2_WAVE) {
-      int ln = lane;
-      asm volatile("" : "+v"(ln));
-      const int cl = ln & (NBF - 1), q = ln >> 2;
-      float acc = 0.0f;
-#pragma unroll
-      for (int i2 = 0; i2 < 4; ++i2) {
-        const int o = 4 * q + i2;
-        const float h = fmaxf(FCP[o * NBF + cl] + FCP[64 * NBF + o * NBF + cl], 0.0f);
-        acc = __builtin_fmaf(buf_load(rs, 16 * q, 4 * (kPkF2 + i2)), h, acc);
-      }
-      acc += __shfl_xor(acc, 4, 64);
-      acc += __shfl_xor(acc, 8, 64);
-      acc += __shfl_xor(acc, 16, 64);
-      acc += __shfl_xor(acc, 32, 64);
-      const int64_t i = b * NBF + cl;
-      if (q == 0 && i < n_mine) logits[clip_base + clip_step * i] = acc;
-    }
+    // No barrier here: classifier.2 of this batch reads the partials after the
+    // next batch's first barrier (below), which already orders them; the
+    // partials are next overwritten three barriers later.
     try_eager(b);
     WK_STAMP(8);
-#ifdef WK_SYNC_AFTER_FC2
+  }
+  if (n_batches > 0) {
     role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);
-#endif
+    fc2(n_batches - 1);
   }
   WK_STAMP_FLUSH(8 + cw);
 }
