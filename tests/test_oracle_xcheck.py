@@ -81,3 +81,28 @@ def test_golden_features_match_third_party(which):
     # tolerance of the GPU tests.
     np.testing.assert_allclose(golden, tp, rtol=0, atol=1e-6)
     np.testing.assert_allclose(O.features_mode_b(x), tp, rtol=0, atol=1e-6)
+
+
+def test_ctc_logmel_matches_third_party():
+    """The CTC head's front-end (X1, ctc.py:82-107: torchaudio MelSpectrogram
+    n_fft 400, hop 160, 80 HTK mels, periodic Hann, centre/reflect, power 2;
+    ln(mel + 1e-8); one global z-score) against the same third-party restatement."""
+    torch = pytest.importorskip("torch")
+    from oracle import wk_ctc_oracle as CO
+    fb = audio_utils.mel_filter_bank(201, 80, 0.0, 8000.0, 16000, norm=None, mel_scale="htk")
+    # (torchaudio, like the oracle, builds the filterbank in float32)
+    np.testing.assert_allclose(CO.mel_fbanks().double().numpy(), fb, rtol=0, atol=1e-5)
+    win = audio_utils.window_function(400, "hann", periodic=True)
+    x = O.synth_clips(77, 0, 3, 48000)
+    ours = CO.features(torch.from_numpy(x).float()).double().numpy()   # (3, T, 80)
+    for u in range(x.shape[0]):
+        mel = audio_utils.spectrogram(x[u].astype(np.float64), win, frame_length=400, hop_length=160,
+                                      fft_length=400, power=2.0, center=True, pad_mode="reflect",
+                                      mel_filters=fb, mel_floor=0.0, dtype=np.float64)   # (80, T)
+        lm = np.log(mel + 1e-8).T
+        lm = (lm - lm.mean()) / lm.std(ddof=1)
+        assert lm.shape == ours[u].shape == (301, 80)
+        # the oracle runs torch.stft in fp32: ~1e-6 typical on unit-scale
+        # z-scores, up to ~3e-4 where a mel band is near the 1e-8 floor
+        err = np.abs(ours[u] - lm)
+        assert np.median(err) < 1e-5 and err.max() < 1e-3, (np.median(err), err.max())
