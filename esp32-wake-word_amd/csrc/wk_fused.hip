@@ -632,7 +632,9 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
         f32x4 m[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#ifndef WK_ABL_NOCONV2
         conv_wino_v<2, F1_CIP, 1>(F1, w2, (cl * I1_TP + 2 * li) * F1_CIP + 4 * lk, m);
+#endif
         epi_wino_pool<F2_CIP, I2_TP, 15>(m, F2, co0, cl, 0, lane);
       }
     }
@@ -670,7 +672,9 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
             for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
           }
           f32x4 m[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#ifndef WK_ABL_NOCONV3   // timing ablations (tools/debug): conv MFMAs skipped (wrong results)
           conv_wino_v<4, F2_CIP, 1>(F2, w3, ((ca + (li >> 3)) * I2_TP + 2 * (li & 7)) * F2_CIP + 4 * lk, m);
+#endif
           epi_wino_gap<NBF>(m, Gp, co0, ca, lane);
           continue;
         }
@@ -696,7 +700,11 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       f32x4 acc = {0, 0, 0, 0};
       const int kh = cw >> 2;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) acc = mfma4(wf1[s], Gp[(64 * kh + 4 * s + lk) * NBF + (li & (NBF - 1))], acc);
+      for (int s = 0; s < 16; ++s) {
+#ifndef WK_ABL_NOFC1
+        acc = mfma4(wf1[s], Gp[(64 * kh + 4 * s + lk) * NBF + (li & (NBF - 1))], acc);
+#endif
+      }
       if (li < NBF) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) FCP[kh * 64 * NBF + (16 * (cw & 3) + 4 * lk + r) * NBF + li] = acc[r];
