@@ -657,7 +657,7 @@ __global__ void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T
 // fragments in VGPRs (kOutRF row tiles x 8 K-steps) and walks V in 64-column tiles of W staged through
 // a double-buffered LDS image (row pitch 264 halfs: the 16 column lanes of a
 // ds_read_b128 land on distinct banks), one barrier per tile.  Each lane keeps
-// a running (max, index) for its 8 rows over its columns, visited in increasing
+// a running (max, index) for its 4 RF rows over its columns, visited in increasing
 // order, then 16-lane shuffles pick the first maximum (torch.max semantics).
 // LOGITS = true also stores fp16 logits for the log_softmax kernel; the argmax
 // is this kernel's in both cases, so tokens do not depend on log-probs being
@@ -665,13 +665,18 @@ __global__ void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T
 // ---------------------------------------------------------------------------
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef WK_OUT_RF
-#define WK_OUT_RF 2      // 16-row MFMA tiles per wave
+#define WK_OUT_RF 3      // 16-row MFMA tiles per wave (argmax-only kernel; the logits-storing one keeps 2: no spills)
 #endif
 #ifndef WK_OUT_WAVES
 #define WK_OUT_WAVES 8
 #endif
 constexpr int kOutK = 2 * kH, kOutBN = 64, kOutPitch = kOutK + 8, kOutRF = WK_OUT_RF, kOutWaves = WK_OUT_WAVES;
-constexpr int kOutRows = 16 * kOutRF * kOutWaves, kOutPre = kOutBN * (kOutK / 8) / (64 * kOutWaves);
+// (RF = 3, 48 rows per wave: each B fragment read from LDS feeds 3 MFMAs -- the
+// LDS bytes per MFMA were the limit at RF = 2; 246 VGPRs, still 2 waves per
+// SIMD: +3 % utterances/s.)
+constexpr int kOutPre = kOutBN * (kOutK / 8) / (64 * kOutWaves);
+constexpr int out_rf(bool logits) { return logits ? 2 : kOutRF; }
+constexpr int out_rows(bool logits) { return 16 * out_rf(logits) * kOutWaves; }
 static_assert(kOutPre * 64 * kOutWaves == kOutBN * (kOutK / 8), "W tile chunks divide over the threads");
 
 template <bool LOGITS>
@@ -680,7 +685,9 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
                                                                           const float* __restrict__ bias, int64_t rows,
                                                                           int V, __half* __restrict__ logits,
                                                                           int* __restrict__ best) {
+  constexpr int kOutRF = out_rf(LOGITS), kOutRows = out_rows(LOGITS);
   __shared__ __attribute__((aligned(16))) _Float16 bt[2][kOutBN * kOutPitch];
+  __shared__ float bsh[2][kOutBN];   // the tile's bias, staged with its W rows (an L2 load per column in the epilogue stalled it)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int64_t row0 = (int64_t)blockIdx.x * kOutRows + 16 * kOutRF * wv;
@@ -699,6 +706,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   const int NT = (V + kOutBN - 1) / kOutBN;
   // W tile nt -> registers: 64 rows x 32 16-byte chunks, 4 per thread
   uint4 pre[kOutPre];
+  float pb = 0.0f;
   auto fetch = [&](int nt) {
 #pragma unroll
     for (int i = 0; i < kOutPre; ++i) {
@@ -706,6 +714,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       const int v = nt * kOutBN + rr;
       pre[i] = v < V ? *reinterpret_cast<const uint4*>(w + (int64_t)v * kOutK + 8 * ch) : make_uint4(0, 0, 0, 0);
     }
+    if (tid < kOutBN) pb = nt * kOutBN + tid < V ? bias[nt * kOutBN + tid] : 0.0f;
   };
   auto stash = [&](int buf) {
 #pragma unroll
@@ -713,6 +722,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
       *reinterpret_cast<uint4*>(&bt[buf][rr * kOutPitch + 8 * ch]) = pre[i];
     }
+    if (tid < kOutBN) bsh[buf][tid] = pb;
   };
   fetch(0);
   stash(0);
@@ -748,7 +758,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     for (int cf = 0; cf < 4; ++cf) {
       const int v = nt * kOutBN + 16 * cf + li;
       if (v < V) {
-        const float bb = bias[v];
+        const float bb = bsh[nt & 1][16 * cf + li];
 #pragma unroll
         for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
@@ -1091,7 +1101,7 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
     }
     if (f16) {
       // fused output layer + argmax; fp16 logits are written only for log_softmax
-      const dim3 og((unsigned)((rows + kOutRows - 1) / kOutRows));
+      const dim3 og((unsigned)((rows + out_rows(d_log_probs != nullptr) - 1) / out_rows(d_log_probs != nullptr)));
       if (d_log_probs) {
         hipLaunchKernelGGL(ctc_out_argmax16_kernel<true>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
                            c->out_b, rows, V, c->logits16, c->best);
