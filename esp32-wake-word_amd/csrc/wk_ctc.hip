@@ -197,6 +197,12 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
   }
 }
 
+// Global z-score of one utterance per block (ctc.py:101-104: mean, unbiased
+// std, applied only when std > 0).  Up to kZsCache float4 per thread stay in
+// registers between the two reductions and the write-back, so the utterance
+// is read from HBM once (it was read three times: 0.27 ms per 4096
+// utterances); longer utterances (> 32,768 values, T > 409) re-read.
+constexpr int kZsCache = 8;
 __global__ __launch_bounds__(1024) void ctc_zscore_kernel(float* __restrict__ feats, int64_t n_per) {
   __shared__ float red[16];
   __shared__ float bc;
@@ -216,6 +222,40 @@ __global__ __launch_bounds__(1024) void ctc_zscore_kernel(float* __restrict__ fe
     __syncthreads();
     return r;
   };
+  const int64_t n4 = n_per / 4;
+  if (n_per % 4 == 0 && n4 <= 1024 * kZsCache && ((uintptr_t)f & 15) == 0) {
+    float4* f4 = reinterpret_cast<float4*>(f);
+    float4 v[kZsCache];
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kZsCache; ++k) {
+      const int64_t i = tid + 1024 * k;
+      v[k] = i < n4 ? f4[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    }
+    const float mean = block_sum(s) / (float)n_per;
+    float q = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kZsCache; ++k) {
+      if (tid + 1024 * k < n4) {
+        const float a = v[k].x - mean, b = v[k].y - mean, c = v[k].z - mean, d = v[k].w - mean;
+        q = __builtin_fmaf(a, a, q);
+        q = __builtin_fmaf(b, b, q);
+        q = __builtin_fmaf(c, c, q);
+        q = __builtin_fmaf(d, d, q);
+      }
+    }
+    const float sd = sqrtf(block_sum(q) / (float)(n_per - 1));
+    if (!(sd > 0.0f)) return;   // ctc.py:101-104: only when std > 0
+    const float inv = 1.0f / sd;
+#pragma unroll
+    for (int k = 0; k < kZsCache; ++k) {
+      const int64_t i = tid + 1024 * k;
+      if (i < n4)
+        f4[i] = make_float4((v[k].x - mean) * inv, (v[k].y - mean) * inv, (v[k].z - mean) * inv, (v[k].w - mean) * inv);
+    }
+    return;
+  }
   float s = 0.0f;
   for (int64_t i = tid; i < n_per; i += 1024) s += f[i];
   const float mean = block_sum(s) / (float)n_per;
@@ -225,7 +265,7 @@ __global__ __launch_bounds__(1024) void ctc_zscore_kernel(float* __restrict__ fe
     q = __builtin_fmaf(d, d, q);
   }
   const float sd = sqrtf(block_sum(q) / (float)(n_per - 1));
-  if (!(sd > 0.0f)) return;   // ctc.py:101-104: only when std > 0
+  if (!(sd > 0.0f)) return;
   const float inv = 1.0f / sd;
   for (int64_t i = tid; i < n_per; i += 1024) f[i] = (f[i] - mean) * inv;
 }
@@ -310,6 +350,99 @@ __global__ __launch_bounds__(256) void ctc_encoder_kernel(const float* __restric
           st_out(out + r * kH + col,
                  fmaxf(__builtin_fmaf((acc[ct][i] - mean[i]) * rs[i], pb[1][col], pb[2][col]), 0.0f));
         }
+      }
+    }
+  }
+}
+
+// fp16 mode (precision 1, "fp16 GEMM operands"): the same Linear 80 -> 128 +
+// LayerNorm + ReLU on v_mfma_f32_16x16x32_f16 -- K = 80 in 3 steps (the last
+// half zero), 24 MFMAs of 16 cycles per 16 rows instead of 160 fp32 MFMAs of 32
+// (the fp32 kernel above ran at ~1/5 of the HBM rate).  W is the A operand and
+// the rows the B operand, so a lane ends with 4 consecutive output columns of
+// one row per column tile: LayerNorm's sums are in-lane plus two shuffles, and
+// each tile leaves as one 8-byte store.  W fragments come from LDS per block
+// (24 KB; keeping them in VGPRs would cost 96 registers and the occupancy).
+typedef _Float16 h8e __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restrict__ in, int64_t rows,
+                                                            const float* __restrict__ w, const float* __restrict__ bias,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, __half* __restrict__ out) {
+  constexpr int KS = 3, CT = kH / 16;
+  __shared__ __attribute__((aligned(16))) h8e wf[KS][CT][64];   // A[col 16 ct + (l&15)][k = 32 s + 8 (l>>4) + j]
+  __shared__ __attribute__((aligned(16))) float pb[3][kH];      // bias, gamma, beta
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < KS * CT * 64; i += 256) {
+    const int st = i / (CT * 64), ct = (i / 64) % CT, l = i & 63;
+    h8e v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 32 * st + 8 * (l >> 4) + j;
+      v[j] = (_Float16)(k < kMels ? w[(16 * ct + (l & 15)) * kMels + k] : 0.0f);
+    }
+    wf[st][ct][l] = v;
+  }
+  for (int i = tid; i < kH; i += 256) {
+    pb[0][i] = bias[i];
+    pb[1][i] = gamma[i];
+    pb[2][i] = beta[i];
+  }
+  __syncthreads();
+  const int li = lane & 15, lg = lane >> 4;
+  const int64_t nblk = (rows + 15) / 16;
+  for (int64_t blk = (int64_t)blockIdx.x * 4 + wv; blk < nblk; blk += (int64_t)gridDim.x * 4) {
+    const int64_t r = blk * 16 + li;   // this lane's row
+    h8e xb[KS];
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int k0 = 32 * st + 8 * lg;
+      float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = a;
+      if (r < rows && k0 < kMels) {
+        const float4* p = reinterpret_cast<const float4*>(in + r * kMels + k0);
+        a = p[0];
+        b = p[1];
+      }
+      xb[st] = h8e{(_Float16)a.x, (_Float16)a.y, (_Float16)a.z, (_Float16)a.w,
+                   (_Float16)b.x, (_Float16)b.y, (_Float16)b.z, (_Float16)b.w};
+    }
+    f32x4 acc[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[ct] = *reinterpret_cast<const f32x4*>(&pb[0][16 * ct + 4 * lg]);   // + bias
+    int wl = lane;
+    asm volatile("" : "+v"(wl));   // W fragments re-read per block, not hoisted into 96 VGPRs
+#pragma unroll
+    for (int st = 0; st < KS; ++st)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[st][ct][wl], xb[st], acc[ct], 0, 0, 0);
+    // acc[ct][i] = row r, column 16 ct + 4 lg + i; the row's 128 columns are in lanes li + 16 q
+    float s1 = 0.0f;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) s1 += (acc[ct][0] + acc[ct][1]) + (acc[ct][2] + acc[ct][3]);
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    const float mean = s1 * (1.0f / kH);
+    float s2 = 0.0f;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d = acc[ct][i] - mean;
+        s2 = __builtin_fmaf(d, d, s2);
+      }
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    const float rs = 1.0f / sqrtf(s2 * (1.0f / kH) + 1e-5f);   // biased variance, as nn.LayerNorm
+    if (r < rows) {
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int c0 = 16 * ct + 4 * lg;
+        const f32x4 g = *reinterpret_cast<const f32x4*>(&pb[1][c0]);
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(&pb[2][c0]);
+        _Float16 y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = (_Float16)fmaxf(__builtin_fmaf((acc[ct][i] - mean) * rs, g[i], bt[i]), 0.0f);
+        *reinterpret_cast<uint2*>(out + r * kH + c0) = __builtin_bit_cast(uint2, y);
       }
     }
   }
@@ -632,20 +765,32 @@ __global__ __launch_bounds__(256) void ctc_argmax_only_kernel(const LT* __restri
   }
 }
 
-__global__ void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T, int* __restrict__ tokens,
-                                  int* __restrict__ lengths) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// decode_predictions (ctc.py:453-471): drop blanks (0) and collapse repeats,
+// prev starting at the blank (ctc.py:462).  One wave per utterance, 64 frames
+// at a time: a frame is kept when tok != 0 and tok != tok[t-1]; its output slot
+// is the count kept so far plus the kept lanes below it (ballot + mbcnt).
+// (One thread per utterance walking its T frames serially took 0.17 ms per
+// 4096 utterances: strided, dependent loads.)
+__global__ __launch_bounds__(256) void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T,
+                                                         int* __restrict__ tokens, int* __restrict__ lengths) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (b >= B) return;
   const int* p = best + b * T;
   int* o = tokens + b * T;
-  int prev = 0, n = 0;   // prev starts at the blank (ctc.py:462)
-  for (int t = 0; t < T; ++t) {
-    const int tok = p[t];
-    if (tok != 0 && tok != prev) o[n++] = tok;
-    prev = tok;
+  int n = 0;
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + lane;
+    const int tok = t < T ? p[t] : 0;
+    const int prev = t == 0 ? 0 : (t < T ? p[t - 1] : 0);
+    const bool keep = tok != 0 && tok != prev;
+    const uint64_t m = __ballot(keep);
+    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    if (keep) o[n + below] = tok;
+    n += __popcll(m);
   }
-  for (int t = n; t < T; ++t) o[t] = -1;
-  lengths[b] = n;
+  for (int t = n + lane; t < T; t += 64) o[t] = -1;
+  if (lane == 0) lengths[b] = n;
 }
 
 // ---------------------------------------------------------------------------
@@ -1075,8 +1220,8 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
     if (rocblas_set_stream(c->blas, st) != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_set_stream");
     const int enc_grid = (int)((rows + 63) / 64 < 8 * c->n_cu ? (rows + 63) / 64 : 8 * c->n_cu);
     if (f16)
-      hipLaunchKernelGGL(ctc_encoder_kernel<__half>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
-                         c->enc_b, c->ln_g, c->ln_b, c->x0h);
+      hipLaunchKernelGGL(ctc_encoder16_kernel, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w, c->enc_b,
+                         c->ln_g, c->ln_b, c->x0h);
     else
       hipLaunchKernelGGL(ctc_encoder_kernel<float>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
                          c->enc_b, c->ln_g, c->ln_b, c->x0);
@@ -1111,7 +1256,7 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
         hipLaunchKernelGGL(ctc_out_argmax16_kernel<false>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
                            c->out_b, rows, V, (__half*)nullptr, c->best);
       }
-      hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st, c->best, batch, T,
+      hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
                          d_tokens, d_lengths);
       e = hipGetLastError();
       return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_forward launch");
@@ -1126,7 +1271,7 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
     else
       hipLaunchKernelGGL(ctc_argmax_kernel<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits,
                          c->out_b, rows, V, d_log_probs, c->best);
-    hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st, c->best, batch, T,
+    hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
                        d_tokens, d_lengths);
     e = hipGetLastError();
     return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_forward launch");
