@@ -26,7 +26,7 @@
 //   ctc_argmax_only_kernel  the same argmax when no log-probs are asked for:
 //                         persistent, bias in LDS, a row's loads issued a row
 //                         ahead, no exp.
-//   ctc_greedy_kernel     one thread per utterance: drop blanks, collapse repeats.
+//   ctc_greedy_kernel     one wave per utterance: drop blanks, collapse repeats.
 #include <stdlib.h>
 #include <string.h>
 
