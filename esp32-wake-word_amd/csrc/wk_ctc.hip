@@ -152,14 +152,23 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
       const int t = (int)(row - b * T);
       const float* xa = audio + b * stride;
       f2 v[20];
+      const int p0 = t * kHop - kNfft / 2;
+      if (p0 >= 0 && p0 + kNfft <= (n_valid < n_pad ? n_valid : n_pad)) {
+        // interior frame inside the valid samples (all but ~2 frames per
+        // utterance): no reflection, no padding -- 20 loads off one address
+        const float* xp = xa + p0 + q;
 #pragma unroll
-      for (int n1 = 0; n1 < 20; ++n1) {
-        const int n = 20 * n1 + q;
-        int p = t * kHop - kNfft / 2 + n;
-        p = p < 0 ? -p : p;
-        p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
-        const float s = p < n_valid ? xa[p] : 0.0f;
-        v[n1] = f2{s * L.win[n], 0.0f};
+        for (int n1 = 0; n1 < 20; ++n1) v[n1] = f2{xp[20 * n1] * L.win[20 * n1 + q], 0.0f};
+      } else {
+#pragma unroll
+        for (int n1 = 0; n1 < 20; ++n1) {
+          const int n = 20 * n1 + q;
+          int p = p0 + n;
+          p = p < 0 ? -p : p;
+          p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
+          const float s = p < n_valid ? xa[p] : 0.0f;
+          v[n1] = f2{s * L.win[n], 0.0f};
+        }
       }
       dft20(v);
 #pragma unroll
