@@ -809,8 +809,8 @@ __global__ __launch_bounds__(256) void ctc_greedy_kernel(const int* __restrict__
 // HBM (they were 2 x 9.9 GB of traffic per 4096 utterances).  A workgroup owns
 // kOutRows rows: each of its kOutWaves waves keeps its 16 kOutRF rows' A
 // fragments in VGPRs (kOutRF row tiles x 8 K-steps) and walks V in 64-column tiles of W staged through
-// a double-buffered LDS image (row pitch 264 halfs: the 16 column lanes of a
-// ds_read_b128 land on distinct banks), one barrier per tile.  Each lane keeps
+// a double-buffered LDS image (512-byte rows, 16-byte chunks XOR-swizzled: a
+// B-fragment ds_read_b128 is conflict-free), one barrier per tile.  Each lane keeps
 // a running (max, index) for its 4 RF rows over its columns, visited in increasing
 // order, then 16-lane shuffles pick the first maximum (torch.max semantics).
 // LOGITS = true also stores fp16 logits for the log_softmax kernel; the argmax
@@ -824,7 +824,13 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef WK_OUT_WAVES
 #define WK_OUT_WAVES 8
 #endif
-constexpr int kOutK = 2 * kH, kOutBN = 64, kOutPitch = kOutK + 8, kOutRF = WK_OUT_RF, kOutWaves = WK_OUT_WAVES;
+constexpr int kOutK = 2 * kH, kOutBN = 64, kOutPitch = kOutK, kOutRF = WK_OUT_RF, kOutWaves = WK_OUT_WAVES;
+// W tile rows are 512 B with their 16-byte chunks XOR-swizzled by the row's
+// low 4 bits (chunk c of row n at c ^ (n & 15)): a ds_read_b128 B fragment
+// (row 16 cf + li, chunk 4 st + lg) then hits 16 distinct 4-bank windows in
+// each of the instruction's four lane groups.  (With the former padded pitch
+// of 264 halfs, 42 % of the kernel's LDS cycles were bank conflicts, PMC.)
+__device__ __forceinline__ int out_chunk(int n, int c) { return c ^ (n & 15); }
 // (RF = 3, 48 rows per wave: each B fragment read from LDS feeds 3 MFMAs -- the
 // LDS bytes per MFMA were the limit at RF = 2; 246 VGPRs, still 2 waves per
 // SIMD: +3 % utterances/s.)
@@ -874,7 +880,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #pragma unroll
     for (int i = 0; i < kOutPre; ++i) {
       const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
-      *reinterpret_cast<uint4*>(&bt[buf][rr * kOutPitch + 8 * ch]) = pre[i];
+      *reinterpret_cast<uint4*>(&bt[buf][rr * kOutPitch + 8 * out_chunk(rr, ch)]) = pre[i];
     }
     if (tid < kOutBN) bsh[buf][tid] = pb;
   };
@@ -890,6 +896,9 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   for (int nt = 0; nt < NT; ++nt) {
     if (nt + 1 < NT) fetch(nt + 1);
     const _Float16* b = bt[nt & 1];
+    float bbc[4];   // the tile's bias, read before the MFMAs (read in the epilogue, its LDS latency was exposed per column tile)
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf) bbc[cf] = bsh[nt & 1][16 * cf + li];
     f32x4 acc[kOutRF][4];
 #pragma unroll
     for (int rf = 0; rf < kOutRF; ++rf)
@@ -900,7 +909,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       h8 bf[4];
 #pragma unroll
       for (int cf = 0; cf < 4; ++cf)
-        bf[cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 32 * st + 8 * lg);
+        bf[cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, 4 * st + lg));
 #pragma unroll
       for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
@@ -912,7 +921,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     for (int cf = 0; cf < 4; ++cf) {
       const int v = nt * kOutBN + 16 * cf + li;
       if (v < V) {
-        const float bb = bsh[nt & 1][16 * cf + li];
+        const float bb = bbc[cf];
 #pragma unroll
         for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll

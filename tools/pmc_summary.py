@@ -39,7 +39,7 @@ def main():
     per, dur = load(d)
     out = {}
     for k, ctrs in per.items():
-        if "wk_" not in k:
+        if "wk_" not in k and "ctc_" not in k and "Cijk" not in k:
             continue
         m = {c: sum(v for _, v in vals) / len(vals) for c, vals in ctrs.items()}
         ns = sum(dur[k].values()) / max(1, len(dur[k]))

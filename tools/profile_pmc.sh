@@ -2,6 +2,7 @@
 # rocprofv3 PMC passes for the bench workload (run on the GPU box via gpurun).
 # Each counter group is its own rocprofv3 run (no --pmc with trace domains).
 #   bash tools/profile_pmc.sh <outdir> [bench args...]
+# (PMC_BENCH=bench_ctc.py profiles the CTC bench instead of bench.py)
 set -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 OUT=${1:-$R/gpurun_out/pmc}; shift
@@ -12,7 +13,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $grp -d "$OUT/p$i" -o run --output-format csv -- python3 "$R/bench.py" $ARGS \
+  timeout -k 10 240 rocprofv3 --pmc $grp -d "$OUT/p$i" -o run --output-format csv -- python3 "$R/${PMC_BENCH:-bench.py}" $ARGS \
     > "$OUT/p$i.log" 2>&1 || { echo "pass $i ($grp) failed rc=$?"; tail -5 "$OUT/p$i.log"; exit 1; }
   echo "pass $i ok: $grp"
 done <<'GROUPS'
