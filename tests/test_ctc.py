@@ -162,3 +162,32 @@ def test_ctc_bit_repeatable_at_scale(precision):
             ref = out
         else:
             assert all(torch.equal(a, b) for a, b in zip(ref, out))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_ctc_long_utterance_and_device_decode(ctc, precision):
+    """8 s utterances (T = 801, Config.max_audio_length): the z-score's
+    streaming path (more values than its register cache holds) and the
+    wave-per-utterance greedy decode across 13 64-frame chunks.  The device
+    tokens must equal decode_predictions applied to the device's own
+    log-probs, and the log-probs must track the oracle."""
+    import wakeword
+    m, _ = ctc
+    g = wakeword.CTCModel(CO.flat_weights(m), V, precision=precision)
+    x = O.synth_clips(17, 0, 3, 128000)
+    feats = g.features(x, n_samples=128000)
+    ref_f = CO.features(torch.from_numpy(x))
+    assert feats.shape == ref_f.shape == (3, 801, 80)
+    assert np.abs(feats.cpu().numpy() - ref_f.numpy()).max() <= FEAT_ATOL
+    seqs, lp = g.forward(feats, return_log_probs=True)
+    lp = lp.cpu()
+    if precision == "fp32":
+        # one kernel computes both the argmax and the log-probs; in fp16 mode the
+        # log-probs come from fp16-rounded logits, so their own argmax can break
+        # near-ties differently from the fp32 accumulators the tokens use
+        assert seqs == CO.greedy_decode(lp)
+    with torch.no_grad():
+        ref_lp = m(ref_f)
+    assert np.abs((lp - ref_lp).numpy()).max() <= (LOGP_ATOL if precision == "fp32" else 0.05)
+    assert seqs == g.forward(feats)   # the argmax-only kernel agrees with the log-prob path
