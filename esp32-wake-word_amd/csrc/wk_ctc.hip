@@ -578,32 +578,48 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const __half* __
   const float* bh = bhh + dir * 3 * kH;
   const float b_r = bi[u] + bh[u], b_z = bi[kH + u] + bh[kH + u], bi_c = bi[2 * kH + u], bh_c = bh[2 * kH + u];
   __half g_r[kSlots], g_z[kSlots], g_c[kSlots];
-  auto load_gates = [&](int step) {
-    const int t = dir == 0 ? step : T - 1 - step;
+  // Per slot, running pointers into gi and out at the current step's row: a
+  // step moves them by one frame (+-768 / +-256 halfs), and a row's three gate
+  // inputs are immediate offsets off one address.  (Recomputing the 64-bit
+  // (b T + t) row addresses per load and store had cost ~60 VALU instructions
+  // per wave and step, a quarter of the step.)
+  const int64_t dstep = dir == 0 ? 1 : -1;
+  const __half* gq[kSlots];
+  __half* oq[kSlots];
+  bool live[kSlots];
+#pragma unroll
+  for (int j = 0; j < kSlots; ++j) {
+    const int n = nb + 6 * j;
+    const int64_t b = b0 + n;
+    live[j] = n < kGruBatch && b < B;
+    const int64_t row = (live[j] ? b : 0) * T + (dir == 0 ? 0 : T - 1);
+    gq[j] = gi + row * (6 * kH) + dir * 3 * kH + u;
+    oq[j] = out + row * (2 * kH) + dir * kH + u;
+  }
+  auto load_gates = [&](int step) {   // gate inputs of `step` (gq at that step's row), then advance
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) {
-      const int n = nb + 6 * j;
-      const int64_t b = b0 + n;
-      if (n < kGruBatch && b < B && step < T) {
-        const __half* g = gi + ((size_t)b * T + t) * (6 * kH) + dir * 3 * kH;
-        g_r[j] = g[u];
-        g_z[j] = g[kH + u];
-        g_c[j] = g[2 * kH + u];
+      if (live[j] && step < T) {
+        g_r[j] = gq[j][0];
+        g_z[j] = gq[j][kH];
+        g_c[j] = gq[j][2 * kH];
       }
+      gq[j] += dstep * (6 * kH);
     }
   };
   load_gates(0);
   int cur = 0;
   for (int step = 0; step < T; ++step) {
-    const int t = dir == 0 ? step : T - 1 - step;
     {
       f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
       const _Float16* hb = h16[cur] + (lane & 15) * kH16P + 4 * (lane >> 4);
+      h4 hv[8];   // all eight B fragments first: one LDS wait instead of four
+#pragma unroll
+      for (int s = 0; s < 8; ++s) hv[s] = *reinterpret_cast<const h4*>(hb + 16 * s);
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        const h4 hv = *reinterpret_cast<const h4*>(hb + 16 * s);
-        acc_a = __builtin_amdgcn_mfma_f32_16x16x16f16(wa[s], hv, acc_a, 0, 0, 0);
-        acc_b = __builtin_amdgcn_mfma_f32_16x16x16f16(wb[s], hv, acc_b, 0, 0, 0);
+        acc_a = __builtin_amdgcn_mfma_f32_16x16x16f16(wa[s], hv[s], acc_a, 0, 0, 0);
+        acc_b = __builtin_amdgcn_mfma_f32_16x16x16f16(wb[s], hv[s], acc_b, 0, 0, 0);
       }
       const int ra = 32 * wave + 4 * (lane >> 4), col = lane & 15;
 #pragma unroll
@@ -617,16 +633,16 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const __half* __
     for (int j = 0; j < kSlots; ++j) {
       const int n = nb + 6 * j;
       if (n >= kGruBatch) continue;
-      const int64_t b = b0 + n;
       float hn = 0.0f;
-      if (b < B) {
+      if (live[j]) {
         const float r = sigm(__half2float(g_r[j]) + gh[u * kHP + n] + b_r);
         const float z = sigm(__half2float(g_z[j]) + gh[(kH + u) * kHP + n] + b_z);
         const float c = tanh_fast(__half2float(g_c[j]) + bi_c + r * (gh[(2 * kH + u) * kHP + n] + bh_c));
         const float hp = hs[cur][u * kHP + n];
         hn = __builtin_fmaf(z, hp - c, c);
-        out[((size_t)b * T + t) * (2 * kH) + dir * kH + u] = __float2half(hn);
+        *oq[j] = __float2half(hn);
       }
+      oq[j] += dstep * (2 * kH);
       hs[cur ^ 1][u * kHP + n] = hn;
       h16[cur ^ 1][n * kH16P + u] = (_Float16)hn;
     }
