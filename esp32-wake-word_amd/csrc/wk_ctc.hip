@@ -840,6 +840,15 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef WK_OUT_WAVES
 #define WK_OUT_WAVES 8
 #endif
+#ifndef WK_OUT_SKEW
+#define WK_OUT_SKEW 1
+#endif
+#ifndef WK_OUT_PRIO
+#define WK_OUT_PRIO 0
+#endif
+#ifndef WK_OUT_AGPR
+#define WK_OUT_AGPR 0
+#endif
 constexpr int kOutK = 2 * kH, kOutBN = 64, kOutPitch = kOutK, kOutRF = WK_OUT_RF, kOutWaves = WK_OUT_WAVES;
 // W tile rows are 512 B with their 16-byte chunks XOR-swizzled by the row's
 // low 4 bits (chunk c of row n at c ^ (n & 15)): a ds_read_b128 B fragment
@@ -909,13 +918,50 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
     for (int i = 0; i < 4; ++i) { mx[rf][i] = -INFINITY; ix[rf][i] = 0; }
+  // Skew (WK_OUT_SKEW): the second half of the waves (4-7, each the partner of
+  // a first-half wave on the same SIMD) runs one tile behind in its epilogue:
+  // per tile it finishes tile nt - 1's argmax first, then issues tile nt's
+  // MFMAs, while the first half issues tile nt's MFMAs and then its epilogue.
+  // The barrier keeps all waves on one tile; the skew puts one wave's epilogue
+  // VALU beside its partner's MFMAs instead of both SIMD waves alternating
+  // all-MFMA and all-VALU phases in step.
+  const bool lag = WK_OUT_SKEW && __builtin_amdgcn_readfirstlane(wv) >= kOutWaves / 2;
+  f32x4 acc[kOutRF][4];
+  float bprev[4];
+  auto epilogue = [&](int tile, const float* bb4) {
+    // column v = 64 tile + 16 cf + li, rows row0 + 16 rf + 4 lg + i
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf) {
+      const int v = tile * kOutBN + 16 * cf + li;
+      if (v < V) {
+        const float bb = bb4[cf];
+#pragma unroll
+        for (int rf = 0; rf < kOutRF; ++rf)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float z = acc[rf][cf][i] + bb;
+            if (z > mx[rf][i]) { mx[rf][i] = z; ix[rf][i] = v; }
+            if (LOGITS) {
+              const int64_t r = row0 + 16 * rf + 4 * lg + i;
+              if (r < rows) logits[r * V + v] = __float2half(acc[rf][cf][i]);
+            }
+          }
+      }
+    }
+  };
+#if WK_OUT_PRIO
+  if (lag) __builtin_amdgcn_s_setprio(1);
+#endif
+#if WK_OUT_AGPR
+  asm volatile("" ::: "a0");
+#endif
   for (int nt = 0; nt < NT; ++nt) {
     if (nt + 1 < NT) fetch(nt + 1);
     const _Float16* b = bt[nt & 1];
     float bbc[4];   // the tile's bias, read before the MFMAs (read in the epilogue, its LDS latency was exposed per column tile)
 #pragma unroll
     for (int cf = 0; cf < 4; ++cf) bbc[cf] = bsh[nt & 1][16 * cf + li];
-    f32x4 acc[kOutRF][4];
+    if (lag && nt > 0) epilogue(nt - 1, bprev);
 #pragma unroll
     for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
@@ -932,28 +978,16 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
         for (int cf = 0; cf < 4; ++cf)
           acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf[cf], acc[rf][cf], 0, 0, 0);
     }
-    // epilogue: column v = 64 nt + 16 cf + li, rows row0 + 16 rf + 4 lg + i
+    if (!lag) {
+      epilogue(nt, bbc);
+    } else {
 #pragma unroll
-    for (int cf = 0; cf < 4; ++cf) {
-      const int v = nt * kOutBN + 16 * cf + li;
-      if (v < V) {
-        const float bb = bbc[cf];
-#pragma unroll
-        for (int rf = 0; rf < kOutRF; ++rf)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float z = acc[rf][cf][i] + bb;
-            if (z > mx[rf][i]) { mx[rf][i] = z; ix[rf][i] = v; }
-            if (LOGITS) {
-              const int64_t r = row0 + 16 * rf + 4 * lg + i;
-              if (r < rows) logits[r * V + v] = __float2half(acc[rf][cf][i]);
-            }
-          }
-      }
+      for (int cf = 0; cf < 4; ++cf) bprev[cf] = bbc[cf];
     }
     if (nt + 1 < NT) stash((nt + 1) & 1);
     __syncthreads();
   }
+  if (lag && NT > 0) epilogue(NT - 1, bprev);
   // first maximum across the 16 column lanes of each row
 #pragma unroll
   for (int rf = 0; rf < kOutRF; ++rf)
