@@ -872,9 +872,12 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
                                                                           int* __restrict__ best) {
   constexpr int kOutRF = out_rf(LOGITS), kOutRows = out_rows(LOGITS);
   __shared__ __attribute__((aligned(16))) _Float16 bt[2][kOutBN * kOutPitch];
-  __shared__ float bsh[2][kOutBN];   // the tile's bias, staged with its W rows (an L2 load per column in the epilogue stalled it)
+  // the tile's bias, staged with its W rows (an L2 load per column in the
+  // epilogue stalled it); replicated x4 so one ds_read_b128 is an MFMA C operand
+  __shared__ f32x4 bsh[2][kOutBN];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
+  const bool wave0 = __builtin_amdgcn_readfirstlane(wv) == 0;
   const int64_t row0 = (int64_t)blockIdx.x * kOutRows + 16 * kOutRF * wv;
   // A fragments: rows row0 + 16 rf + li, k = 32 s + 8 lg .. +7
   h8 a[kOutRF][8];
@@ -889,17 +892,20 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     }
   }
   const int NT = (V + kOutBN - 1) / kOutBN;
-  // W tile nt -> registers: 64 rows x 32 16-byte chunks, 4 per thread
+  // W tile nt -> registers: 64 rows x 32 16-byte chunks, 4 per thread.  Buffer
+  // loads: rows past V come back 0 from the range check, no branch per load.
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(w, (uint32_t)V * kOutK * 2);
+  const __amdgpu_buffer_rsrc_t brs = make_rsrc(bias, (uint32_t)V * 4);
   uint4 pre[kOutPre];
   float pb = 0.0f;
   auto fetch = [&](int nt) {
 #pragma unroll
     for (int i = 0; i < kOutPre; ++i) {
       const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
-      const int v = nt * kOutBN + rr;
-      pre[i] = v < V ? *reinterpret_cast<const uint4*>(w + (int64_t)v * kOutK + 8 * ch) : make_uint4(0, 0, 0, 0);
+      pre[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             wrs, (nt * kOutBN + rr) * (kOutK * 2) + 16 * ch, 0, 0));
     }
-    if (tid < kOutBN) pb = nt * kOutBN + tid < V ? bias[nt * kOutBN + tid] : 0.0f;
+    if (wave0) pb = buf_load(brs, 4 * (nt * kOutBN + tid), 0);
   };
   auto stash = [&](int buf) {
 #pragma unroll
@@ -907,7 +913,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
       *reinterpret_cast<uint4*>(&bt[buf][rr * kOutPitch + 8 * out_chunk(rr, ch)]) = pre[i];
     }
-    if (tid < kOutBN) bsh[buf][tid] = pb;
+    if (wave0) bsh[buf][tid] = f32x4{pb, pb, pb, pb};
   };
   fetch(0);
   stash(0);
@@ -926,6 +932,10 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   // VALU beside its partner's MFMAs instead of both SIMD waves alternating
   // all-MFMA and all-VALU phases in step.
   const bool lag = WK_OUT_SKEW && __builtin_amdgcn_readfirstlane(wv) >= kOutWaves / 2;
+  // Argmax-only: the bias is the MFMAs' initial C operand (one ds_read_b128 of
+  // the replicated bias per column tile), so the epilogue is compare + select.
+  // LOGITS stores the bias-free logits (log_softmax adds it) and adds it here.
+  constexpr bool kBiasAcc = !LOGITS;
   f32x4 acc[kOutRF][4];
   float bprev[4];
   auto epilogue = [&](int tile, const float* bb4) {
@@ -934,12 +944,11 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     for (int cf = 0; cf < 4; ++cf) {
       const int v = tile * kOutBN + 16 * cf + li;
       if (v < V) {
-        const float bb = bb4[cf];
 #pragma unroll
         for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float z = acc[rf][cf][i] + bb;
+            const float z = kBiasAcc ? acc[rf][cf][i] : acc[rf][cf][i] + bb4[cf];
             if (z > mx[rf][i]) { mx[rf][i] = z; ix[rf][i] = v; }
             if (LOGITS) {
               const int64_t r = row0 + 16 * rf + 4 * lg + i;
@@ -952,35 +961,40 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #if WK_OUT_PRIO
   if (lag) __builtin_amdgcn_s_setprio(1);
 #endif
-#if WK_OUT_AGPR
-  asm volatile("" ::: "a0");
-#endif
   for (int nt = 0; nt < NT; ++nt) {
     if (nt + 1 < NT) fetch(nt + 1);
     const _Float16* b = bt[nt & 1];
-    float bbc[4];   // the tile's bias, read before the MFMAs (read in the epilogue, its LDS latency was exposed per column tile)
+    float bbc[4];   // LOGITS: the tile's bias for the epilogue add
+    if (!kBiasAcc) {
 #pragma unroll
-    for (int cf = 0; cf < 4; ++cf) bbc[cf] = bsh[nt & 1][16 * cf + li];
+      for (int cf = 0; cf < 4; ++cf) bbc[cf] = bsh[nt & 1][16 * cf + li][0];
+    }
     if (lag && nt > 0) epilogue(nt - 1, bprev);
-#pragma unroll
-    for (int rf = 0; rf < kOutRF; ++rf)
-#pragma unroll
-      for (int cf = 0; cf < 4; ++cf) acc[rf][cf] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       h8 bf[4];
 #pragma unroll
       for (int cf = 0; cf < 4; ++cf)
         bf[cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, 4 * st + lg));
+      if (st == 0) {
 #pragma unroll
-      for (int rf = 0; rf < kOutRF; ++rf)
+        for (int cf = 0; cf < 4; ++cf) {
+          const f32x4 c0 = kBiasAcc ? bsh[nt & 1][16 * cf + li] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int cf = 0; cf < 4; ++cf)
-          acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf[cf], acc[rf][cf], 0, 0, 0);
+          for (int rf = 0; rf < kOutRF; ++rf)
+            acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][0], bf[cf], c0, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int rf = 0; rf < kOutRF; ++rf)
+#pragma unroll
+          for (int cf = 0; cf < 4; ++cf)
+            acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf[cf], acc[rf][cf], 0, 0, 0);
+      }
     }
     if (!lag) {
       epilogue(nt, bbc);
-    } else {
+    } else if (!kBiasAcc) {
 #pragma unroll
       for (int cf = 0; cf < 4; ++cf) bprev[cf] = bbc[cf];
     }
