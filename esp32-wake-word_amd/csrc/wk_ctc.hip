@@ -62,16 +62,27 @@ constexpr int kNfft = 400, kHop = 160, kBins = kNfft / 2 + 1, kMels = 80, kH = 1
 // instead of the 321 kflop of the DFT-as-GEMM it replaces.
 // ---------------------------------------------------------------------------
 constexpr int kFftWaves = 4, kFftFrames = 3;           // frames per wave pass
-constexpr int kAPitch = 11;                             // A[f][n2][k1], k1 = 0..10 (float2)
-constexpr int kPwPitch = 204;
+// LDS pitches (float2 / float units) chosen so that every wave-wide access is
+// bank-conflict-free for the 3-frame lane layout (lanes 0-19, 20-39, 40-59):
+// A rows of 15 float2 (stage-1 ds_write_b64 and stage-2 ds_read_b64 both), twiddle
+// rows of 21 float2 (stage-2 reads, lane = k1), power rows of 212 floats (212 = 20
+// mod 64: the three frames' 20-lane writes fill disjoint bank ranges).  With 11 /
+// 20 / 204, 45 % of the kernel's LDS cycles were conflicts (PMC).
+constexpr int kAPitch = 15;                             // A[f][n2][k1], k1 = 0..10 (float2)
+constexpr int kTwPitch = 21;
+constexpr int kPwPitch = 212;
 constexpr int kFbMaxW = 640;                           // CSR mel weights kept in LDS (host checks nnz)
 struct CtcFftLds {
   float fbw[kFbMaxW];
   int fbs[kMels], fbl[kMels], fbo[kMels];
   float win[kNfft];
-  f2 tw[20][20];                                        // W400^(n2 k1), [k1][n2]
-  f2 a[kFftWaves][kFftFrames * 20 * kAPitch];
-  float pw[kFftWaves][kFftFrames][kPwPitch];
+  f2 tw[20][kTwPitch];                                  // W400^(n2 k1), [k1][n2]
+  // per wave: the stage-1 -> stage-2 matrix, and the power rows written by
+  // stage 2 after its last read of it (one wave's LDS ops complete in order)
+  union {
+    f2 a[kFftFrames * 20 * kAPitch];
+    float pw[kFftFrames][kPwPitch];
+  } w[kFftWaves];
 };
 
 // W20^e = exp(-2 pi i e / 20).
@@ -140,37 +151,60 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int f = lane / 20, q = lane - 20 * (lane / 20);   // frame slot (3 = idle lanes 60-63), n2 / k1
-  f2* A = L.a[wv];
-  float* PW = &L.pw[wv][0][0];
+  f2* A = L.w[wv].a;
+  float* PW = &L.w[wv].pw[0][0];
   const int64_t passes = (rows + kFftFrames - 1) / kFftFrames;
-  for (int64_t ps = (int64_t)blockIdx.x * kFftWaves + wv; ps < passes; ps += (int64_t)gridDim.x * kFftWaves) {
+  const int64_t pstep = (int64_t)gridDim.x * kFftWaves;
+  // The lane's 20 samples x[20 n1 + q] of pass ps_'s frame f: the next pass's
+  // are loaded while this pass's FFTs and mel run.  Both paths are wave-uniform
+  // and issue exactly 20 loads with no per-lane branch, so the compiler's load
+  // counter stays exact across the loop (a per-lane branch made it wait for the
+  // prefetch before stage 1).  Idle lanes read the first samples of utterance 0
+  // on the interior path; nothing they compute is stored.
+  const int nv_min = n_valid < n_pad ? n_valid : n_pad;
+  auto load_raw = [&](int64_t ps_, float (&raw)[20]) {
+    const int64_t row = ps_ * kFftFrames + f;
+    const bool live = f < kFftFrames && ps_ < passes && row < rows;
+    const int rr = live ? (int)row : 0;   // rows < 2^31 (host check)
+    const int b = (int)((unsigned)rr / (unsigned)T), t = rr - b * T;
+    const float* xa = audio + (int64_t)b * stride;
+    const int p0 = live ? t * kHop - kNfft / 2 : 0;
+    if (__all(p0 >= 0 && p0 + kNfft <= nv_min)) {
+      // interior frames inside the valid samples (all but ~2 frames per
+      // utterance): no reflection, no padding -- 20 loads off one address
+      const float* xp = xa + p0 + q;
+#pragma unroll
+      for (int n1 = 0; n1 < 20; ++n1) raw[n1] = xp[20 * n1];
+    } else {
+#pragma unroll
+      for (int n1 = 0; n1 < 20; ++n1) {
+        int p = p0 + 20 * n1 + q;
+        p = p < 0 ? -p : p;
+        p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
+        const bool in = p < n_valid;
+        const float x = xa[in ? p : 0];
+        raw[n1] = in ? x : 0.0f;
+      }
+    }
+  };
+  float raw[20];
+  load_raw((int64_t)blockIdx.x * kFftWaves + wv, raw);
+  for (int64_t ps = (int64_t)blockIdx.x * kFftWaves + wv; ps < passes; ps += pstep) {
     const int64_t row = ps * kFftFrames + f;
     const bool act = f < kFftFrames && row < rows;
     // stage 1: lane (f, n2 = q): DFT-20 over n1 of x[20 n1 + n2]
+    f2 v[20];
+#pragma unroll
+    for (int n1 = 0; n1 < 20; ++n1) {
+      v[n1] = f2{raw[n1] * L.win[20 * n1 + q], 0.0f};
+      // pin the product here, ahead of the next pass's loads: otherwise it sinks
+      // into the stage-1 block, the old and new samples are live together and
+      // the loop-carried copies make every pass wait for its own prefetch
+      asm volatile("" ::"v"(v[n1].x) : "memory");
+    }
+    load_raw(ps + pstep, raw);
+    dft20(v);
     if (act) {
-      const int64_t b = row / T;
-      const int t = (int)(row - b * T);
-      const float* xa = audio + b * stride;
-      f2 v[20];
-      const int p0 = t * kHop - kNfft / 2;
-      if (p0 >= 0 && p0 + kNfft <= (n_valid < n_pad ? n_valid : n_pad)) {
-        // interior frame inside the valid samples (all but ~2 frames per
-        // utterance): no reflection, no padding -- 20 loads off one address
-        const float* xp = xa + p0 + q;
-#pragma unroll
-        for (int n1 = 0; n1 < 20; ++n1) v[n1] = f2{xp[20 * n1] * L.win[20 * n1 + q], 0.0f};
-      } else {
-#pragma unroll
-        for (int n1 = 0; n1 < 20; ++n1) {
-          const int n = 20 * n1 + q;
-          int p = p0 + n;
-          p = p < 0 ? -p : p;
-          p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
-          const float s = p < n_valid ? xa[p] : 0.0f;
-          v[n1] = f2{s * L.win[n], 0.0f};
-        }
-      }
-      dft20(v);
 #pragma unroll
       for (int k1 = 0; k1 <= 10; ++k1) A[(f * 20 + q) * kAPitch + k1] = v[k1];
     }
@@ -1255,14 +1289,18 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
   if (batch == 0) return WK_OK;
   const int T = 1 + n_samples / kHop;
   const int64_t rows = batch * (int64_t)T;
+  if (rows > INT32_MAX) return invalid("wk_ctc_features: batch x frames exceeds 2^31 rows");
   return on_device(c->cfg.device, [&]() -> wk_status {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     const int nv = n_valid < n_samples ? n_valid : n_samples;
     const int64_t passes = (rows + kFftFrames - 1) / kFftFrames;
     const int64_t blocks = (passes + kFftWaves - 1) / kFftWaves;
+    // n_valid == 0: every sample is padding; the kernel's (masked) loads then
+    // read a device table instead of a possibly empty audio buffer
+    const float* au = nv > 0 ? d_audio : c->fft_win;
     hipLaunchKernelGGL(ctc_logmel_fft_kernel, dim3((unsigned)(blocks < 8 * c->n_cu ? blocks : 8 * c->n_cu)), dim3(256), 0,
-                       st, d_audio, stride, nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->fb_start, c->fb_len,
+                       st, au, nv > 0 ? stride : (int64_t)0, nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->fb_start, c->fb_len,
                        c->fb_off, c->fb_w, c->n_fbw, d_feats);
     hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
     e = hipGetLastError();
