@@ -407,10 +407,14 @@ __global__ __launch_bounds__(256) void ctc_encoder_kernel(const float* __restric
 // each tile leaves as one 8-byte store.  W fragments come from LDS per block
 // (24 KB; keeping them in VGPRs would cost 96 registers and the occupancy).
 typedef _Float16 h8e __attribute__((ext_vector_type(8)));
+// Output rows are time-major (row t B + b for input row b T + t): the fp16
+// path keeps every [rows][.] tensor after the encoder in that order, so that a
+// GRU step's 16 utterances are 16 adjacent rows of the gate inputs and outputs.
 __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restrict__ in, int64_t rows,
                                                             const float* __restrict__ w, const float* __restrict__ bias,
                                                             const float* __restrict__ gamma,
-                                                            const float* __restrict__ beta, __half* __restrict__ out) {
+                                                            const float* __restrict__ beta, int B, int T,
+                                                            __half* __restrict__ out) {
   constexpr int KS = 3, CT = kH / 16;
   __shared__ __attribute__((aligned(16))) h8e wf[KS][CT][64];   // A[col 16 ct + (l&15)][k = 32 s + 8 (l>>4) + j]
   __shared__ __attribute__((aligned(16))) float pb[3][kH];      // bias, gamma, beta
@@ -477,6 +481,8 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
     s2 += __shfl_xor(s2, 32, 64);
     const float rs = 1.0f / sqrtf(s2 * (1.0f / kH) + 1e-5f);   // biased variance, as nn.LayerNorm
     if (r < rows) {
+      const int ub = (int)r / T, ut = (int)r - ub * T;   // rows < 2^31 (host check)
+      __half* orow = out + ((int64_t)ut * B + ub) * kH;
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         const int c0 = 16 * ct + 4 * lg;
@@ -485,7 +491,7 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
         _Float16 y[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) y[i] = (_Float16)fmaxf(__builtin_fmaf((acc[ct][i] - mean) * rs, g[i], bt[i]), 0.0f);
-        *reinterpret_cast<uint2*>(out + r * kH + c0) = __builtin_bit_cast(uint2, y);
+        *reinterpret_cast<uint2*>(orow + c0) = __builtin_bit_cast(uint2, y);
       }
     }
   }
@@ -577,112 +583,133 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru_kernel(const float* __res
 // gates and the state update stay fp32.  A fragment of tile tl, k-step s:
 // lane l holds W[16 tl + (l & 15)][16 s + 4 (l >> 4) + j], j = 0..3; the B
 // fragment is h16[batch = l & 15][16 s + 4 (l >> 4) + j] from LDS (one b64 read).
+//
+// Wave w computes the r, z and n tiles of the same 16 units (tiles w, 8 + w,
+// 16 + w), so a lane's three accumulators hold gh_r, gh_z, gh_n of units
+// 16 w + 4 (l >> 4) + i (i = 0..3) for batch slot l & 15: the gates, the state
+// update and the fp32 state itself stay in its registers.  A step is 24 MFMAs,
+// the gate math for 4 elements, one 8-byte LDS write of the new fp16 state and
+// one barrier per wave.  (The previous layout -- 32 consecutive gate rows per
+// wave, gh and the fp32 state through LDS, 12 waves -- issued ~2.6x the
+// instructions per step and needed two barriers.)
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 constexpr int kH16P = kH + 4;   // LDS pitch (halves) of the fp16 state image [batch][unit]
+constexpr int kGru16Waves = kH / 16, kGru16Threads = 64 * kGru16Waves;
+#ifndef WK_GRU_PF
+#define WK_GRU_PF 3
+#endif
+constexpr int kGruPf = WK_GRU_PF;
+#ifndef WK_GRU_ABL
+#define WK_GRU_ABL 0
+#endif   // gate-input prefetch depth (steps)
 
-__global__ __launch_bounds__(kGruThreads) void ctc_gru16_kernel(const __half* __restrict__ gi, const h4* __restrict__ whh_pk,
-                                                                const float* __restrict__ bih,
-                                                                const float* __restrict__ bhh, int64_t B, int T,
-                                                                __half* __restrict__ out) {   // fp16: the next GEMM's operand
-  __shared__ float hs[2][kH * kHP];
-  __shared__ float gh[3 * kH * kHP];
+__global__ __launch_bounds__(kGru16Threads) void ctc_gru16_kernel(const __half* __restrict__ gi, const h4* __restrict__ whh_pk,
+                                                                  const float* __restrict__ bih,
+                                                                  const float* __restrict__ bhh, int64_t B, int T,
+                                                                  __half* __restrict__ out) {   // fp16: the next GEMM's operand
   __shared__ __attribute__((aligned(16))) _Float16 h16[2][kGruBatch * kH16P];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int dir = blockIdx.y;
-  const int64_t b0 = (int64_t)blockIdx.x * kGruBatch;
-  h4 wa[8], wb[8];
+  const int n = lane & 15;                    // batch slot
+  const int u0 = 16 * wave + 4 * (lane >> 4); // the lane's units u0 .. u0 + 3
+  const int64_t b = (int64_t)blockIdx.x * kGruBatch + n;
+  const bool live = b < B;
+  h4 wr[8], wz[8], wn[8];
   {
-    const h4* p = whh_pk + ((size_t)dir * 24 + 2 * wave) * 8 * 64 + lane;
+    const h4* p = whh_pk + (size_t)dir * 24 * 8 * 64 + lane;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      wa[s] = p[s * 64];
-      wb[s] = p[(8 + s) * 64];
+      wr[s] = p[((0 * 8 + wave) * 8 + s) * 64];
+      wz[s] = p[((1 * 8 + wave) * 8 + s) * 64];
+      wn[s] = p[((2 * 8 + wave) * 8 + s) * 64];
     }
   }
-  for (int i = tid; i < kH * kHP; i += kGruThreads) hs[0][i] = 0.0f;
-  for (int i = tid; i < kGruBatch * kH16P; i += kGruThreads) h16[0][i] = (_Float16)0.0f;
-  __syncthreads();
-  // Each thread owns one unit u and the batch slots n = nb + 6 j (768 = 6 x 128):
-  // its biases live in registers, and its fp16 gate inputs for step + 1 are
-  // loaded while step's MFMAs run (they do not depend on the recurrence).
-  const int u = tid & (kH - 1), nb = tid >> 7;
-  constexpr int kSlots = (kGruBatch + 5) / 6;
+  for (int i = tid; i < kGruBatch * kH16P; i += kGru16Threads) h16[0][i] = (_Float16)0.0f;
   const float* bi = bih + dir * 3 * kH;
   const float* bh = bhh + dir * 3 * kH;
-  const float b_r = bi[u] + bh[u], b_z = bi[kH + u] + bh[kH + u], bi_c = bi[2 * kH + u], bh_c = bh[2 * kH + u];
-  __half g_r[kSlots], g_z[kSlots], g_c[kSlots];
-  // Per slot, running pointers into gi and out at the current step's row: a
-  // step moves them by one frame (+-768 / +-256 halfs), and a row's three gate
-  // inputs are immediate offsets off one address.  (Recomputing the 64-bit
-  // (b T + t) row addresses per load and store had cost ~60 VALU instructions
-  // per wave and step, a quarter of the step.)
-  const int64_t dstep = dir == 0 ? 1 : -1;
-  const __half* gq[kSlots];
-  __half* oq[kSlots];
-  bool live[kSlots];
+  float b_r[4], b_z[4], bi_c[4], bh_c[4], h[4];
 #pragma unroll
-  for (int j = 0; j < kSlots; ++j) {
-    const int n = nb + 6 * j;
-    const int64_t b = b0 + n;
-    live[j] = n < kGruBatch && b < B;
-    const int64_t row = (live[j] ? b : 0) * T + (dir == 0 ? 0 : T - 1);
-    gq[j] = gi + row * (6 * kH) + dir * 3 * kH + u;
-    oq[j] = out + row * (2 * kH) + dir * kH + u;
+  for (int i = 0; i < 4; ++i) {
+    const int u = u0 + i;
+    b_r[i] = bi[u] + bh[u];
+    b_z[i] = bi[kH + u] + bh[kH + u];
+    bi_c[i] = bi[2 * kH + u];
+    bh_c[i] = bh[2 * kH + u];
+    h[i] = 0.0f;
   }
-  auto load_gates = [&](int step) {   // gate inputs of `step` (gq at that step's row), then advance
-#pragma unroll
-    for (int j = 0; j < kSlots; ++j) {
-      if (live[j] && step < T) {
-        g_r[j] = gq[j][0];
-        g_z[j] = gq[j][kH];
-        g_c[j] = gq[j][2 * kH];
-      }
-      gq[j] += dstep * (6 * kH);
-    }
+  // Running pointers at the current step's row (a step moves them by one
+  // frame, +-768 / +-256 halfs).  A row's three gate inputs for the lane's 4
+  // units are three 8-byte loads, issued kGruPf steps ahead into a ring of
+  // registers (one step ahead left every step waiting on the load latency).
+  // The loads are unconditional -- idle lanes read utterance 0, and past the
+  // last step the pointer stays on the last row -- so no branch splits the
+  // load counter's view of the ring.
+  // gi and out are time-major (row t B + b): a step moves by B rows.
+  const int64_t dstep = dir == 0 ? B : -B;
+  const int64_t row = (int64_t)(dir == 0 ? 0 : T - 1) * B + (live ? b : 0);
+  const __half* gq = gi + row * (6 * kH) + dir * 3 * kH + u0;
+  __half* oq = out + row * (2 * kH) + dir * kH + u0;
+  uint2 g_r[kGruPf], g_z[kGruPf], g_c[kGruPf];
+  auto load_gates = [&](int j, int step) {   // gate inputs of `step` into ring slot j, then advance
+    g_r[j] = *reinterpret_cast<const uint2*>(gq);
+    g_z[j] = *reinterpret_cast<const uint2*>(gq + kH);
+    g_c[j] = *reinterpret_cast<const uint2*>(gq + 2 * kH);
+    gq += step + 1 < T ? dstep * (6 * kH) : 0;
   };
-  load_gates(0);
+#pragma unroll
+  for (int j = 0; j < kGruPf; ++j) load_gates(j, j);
+  __syncthreads();
   int cur = 0;
-  for (int step = 0; step < T; ++step) {
+  for (int step0 = 0; step0 < T; step0 += kGruPf) {
+#pragma unroll
+  for (int j = 0; j < kGruPf; ++j) {
+    const int step = step0 + j;
+    if (step >= T) break;
+    f32x4 ar = {0, 0, 0, 0}, az = {0, 0, 0, 0}, an = {0, 0, 0, 0};
     {
-      f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
-      const _Float16* hb = h16[cur] + (lane & 15) * kH16P + 4 * (lane >> 4);
-      h4 hv[8];   // all eight B fragments first: one LDS wait instead of four
+      const _Float16* hb = h16[cur] + n * kH16P + 4 * (lane >> 4);
+      h4 hv[8];   // all eight B fragments first: one LDS wait
 #pragma unroll
       for (int s = 0; s < 8; ++s) hv[s] = *reinterpret_cast<const h4*>(hb + 16 * s);
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        acc_a = __builtin_amdgcn_mfma_f32_16x16x16f16(wa[s], hv[s], acc_a, 0, 0, 0);
-        acc_b = __builtin_amdgcn_mfma_f32_16x16x16f16(wb[s], hv[s], acc_b, 0, 0, 0);
-      }
-      const int ra = 32 * wave + 4 * (lane >> 4), col = lane & 15;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        gh[(ra + r) * kHP + col] = acc_a[r];
-        gh[(ra + 16 + r) * kHP + col] = acc_b[r];
+        ar = __builtin_amdgcn_mfma_f32_16x16x16f16(wr[s], hv[s], ar, 0, 0, 0);
+        az = __builtin_amdgcn_mfma_f32_16x16x16f16(wz[s], hv[s], az, 0, 0, 0);
+        an = __builtin_amdgcn_mfma_f32_16x16x16f16(wn[s], hv[s], an, 0, 0, 0);
       }
     }
-    __syncthreads();
+    const h4 gr = __builtin_bit_cast(h4, g_r[j]), gz = __builtin_bit_cast(h4, g_z[j]), gc = __builtin_bit_cast(h4, g_c[j]);
+#if WK_GRU_ABL != 2
+    load_gates(j, step + kGruPf);
+#endif
+    h4 o;
 #pragma unroll
-    for (int j = 0; j < kSlots; ++j) {
-      const int n = nb + 6 * j;
-      if (n >= kGruBatch) continue;
+    for (int i = 0; i < 4; ++i) {
       float hn = 0.0f;
-      if (live[j]) {
-        const float r = sigm(__half2float(g_r[j]) + gh[u * kHP + n] + b_r);
-        const float z = sigm(__half2float(g_z[j]) + gh[(kH + u) * kHP + n] + b_z);
-        const float c = tanh_fast(__half2float(g_c[j]) + bi_c + r * (gh[(2 * kH + u) * kHP + n] + bh_c));
-        const float hp = hs[cur][u * kHP + n];
-        hn = __builtin_fmaf(z, hp - c, c);
-        *oq[j] = __float2half(hn);
+      if (live) {
+#if WK_GRU_ABL == 1   // timing ablation: no transcendentals (wrong results)
+        const float r = 0.5f * ((float)gr[i] + ar[i] + b_r[i]);
+        const float z = 0.5f * ((float)gz[i] + az[i] + b_z[i]);
+        const float c = 0.25f * ((float)gc[i] + bi_c[i] + r * (an[i] + bh_c[i]));
+#else
+        const float r = sigm((float)gr[i] + ar[i] + b_r[i]);
+        const float z = sigm((float)gz[i] + az[i] + b_z[i]);
+        const float c = tanh_fast((float)gc[i] + bi_c[i] + r * (an[i] + bh_c[i]));
+#endif
+        hn = __builtin_fmaf(z, h[i] - c, c);   // (1 - z) c + z h
       }
-      oq[j] += dstep * (2 * kH);
-      hs[cur ^ 1][u * kHP + n] = hn;
-      h16[cur ^ 1][n * kH16P + u] = (_Float16)hn;
+      h[i] = hn;
+      o[i] = (_Float16)hn;
     }
-    load_gates(step + 1);
+#if WK_GRU_ABL != 3
+    if (live) *reinterpret_cast<uint2*>(oq) = __builtin_bit_cast(uint2, o);
+#endif
+    oq += dstep * (2 * kH);
+    *reinterpret_cast<uint2*>(&h16[cur ^ 1][n * kH16P + u0]) = __builtin_bit_cast(uint2, o);
     cur ^= 1;
     __syncthreads();
+  }
   }
 }
 
@@ -709,10 +736,11 @@ template <typename LT> struct Vec;
 template <> struct Vec<__half> { static constexpr int N = 8; };
 template <> struct Vec<float> { static constexpr int N = 4; };
 
+// tm_B > 0: logits rows are time-major (t tm_B + b); log_probs stays [b][t].
 template <typename LT>
 __global__ __launch_bounds__(256) void ctc_argmax_kernel(const LT* __restrict__ logits, const float* __restrict__ bias,
                                                          int64_t rows, int V, float* __restrict__ log_probs,
-                                                         int* __restrict__ best) {
+                                                         int* __restrict__ best, int tm_B = 0, int T = 0) {
   constexpr int NV = Vec<LT>::N;   // elements per 16-byte load
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -760,7 +788,8 @@ __global__ __launch_bounds__(256) void ctc_argmax_kernel(const LT* __restrict__ 
   }
   if (log_probs) {
     const float lse = mx + logf(s);
-    for (int v = lane; v < V; v += 64) log_probs[r * V + v] = (float)x[v] + bias[v] - lse;
+    const int64_t orow = tm_B > 0 ? (r % tm_B) * T + r / tm_B : r;
+    for (int v = lane; v < V; v += 64) log_probs[orow * V + v] = (float)x[v] + bias[v] - lse;
   }
   if (lane == 0 && best) best[r] = arg;
 }
@@ -830,18 +859,21 @@ __global__ __launch_bounds__(256) void ctc_argmax_only_kernel(const LT* __restri
 // is the count kept so far plus the kept lanes below it (ballot + mbcnt).
 // (One thread per utterance walking its T frames serially took 0.17 ms per
 // 4096 utterances: strided, dependent loads.)
+// tm: best is time-major (frame t of utterance b at t B + b).
 __global__ __launch_bounds__(256) void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T,
-                                                         int* __restrict__ tokens, int* __restrict__ lengths) {
+                                                         int* __restrict__ tokens, int* __restrict__ lengths,
+                                                         int tm = 0) {
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (b >= B) return;
-  const int* p = best + b * T;
+  const int64_t ts = tm ? B : 1;   // frame stride
+  const int* p = best + (tm ? b : b * T);
   int* o = tokens + b * T;
   int n = 0;
   for (int t0 = 0; t0 < T; t0 += 64) {
     const int t = t0 + lane;
-    const int tok = t < T ? p[t] : 0;
-    const int prev = t == 0 ? 0 : (t < T ? p[t - 1] : 0);
+    const int tok = t < T ? p[t * ts] : 0;
+    const int prev = t == 0 ? 0 : (t < T ? p[(t - 1) * ts] : 0);
     const bool keep = tok != 0 && tok != prev;
     const uint64_t m = __ballot(keep);
     const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -1315,6 +1347,7 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
   if (batch == 0) return WK_OK;
   const int V = c->cfg.vocab, H = kH;
   const int64_t rows = batch * (int64_t)T;
+  if (rows > INT32_MAX) return invalid("wk_ctc_forward: batch x frames exceeds 2^31 rows");
   const bool f16 = c->f16;
   return on_device(c->cfg.device, [&]() -> wk_status {
     hipStream_t st = (hipStream_t)stream;
@@ -1341,7 +1374,7 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
     const int enc_grid = (int)((rows + 63) / 64 < 8 * c->n_cu ? (rows + 63) / 64 : 8 * c->n_cu);
     if (f16)
       hipLaunchKernelGGL(ctc_encoder16_kernel, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w, c->enc_b,
-                         c->ln_g, c->ln_b, c->x0h);
+                         c->ln_g, c->ln_b, (int)batch, T, c->x0h);   // fp16 path: time-major rows from here on
     else
       hipLaunchKernelGGL(ctc_encoder_kernel<float>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
                          c->enc_b, c->ln_g, c->ln_b, c->x0);
@@ -1356,7 +1389,7 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
       if (s != WK_OK) return s;
       const dim3 gg((unsigned)((batch + kGruBatch - 1) / kGruBatch), 2);
       if (f16)
-        hipLaunchKernelGGL(ctc_gru16_kernel, gg, dim3(kGruThreads), 0, st, (const __half*)c->gi, (const h4*)c->whh16_pk[l], c->bih[l],
+        hipLaunchKernelGGL(ctc_gru16_kernel, gg, dim3(kGru16Threads), 0, st, (const __half*)c->gi, (const h4*)c->whh16_pk[l], c->bih[l],
                            c->bhh[l], batch, T, ys16[l]);
       else
         hipLaunchKernelGGL(ctc_gru_kernel, gg, dim3(kGruThreads), 0, st, c->gi, c->whh_pk[l], c->bih[l], c->bhh[l],
@@ -1371,13 +1404,13 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
         hipLaunchKernelGGL(ctc_out_argmax16_kernel<true>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
                            c->out_b, rows, V, c->logits16, c->best);
         hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits16,
-                           c->out_b, rows, V, d_log_probs, (int*)nullptr);
+                           c->out_b, rows, V, d_log_probs, (int*)nullptr, (int)batch, T);
       } else {
         hipLaunchKernelGGL(ctc_out_argmax16_kernel<false>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
                            c->out_b, rows, V, (__half*)nullptr, c->best);
       }
       hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
-                         d_tokens, d_lengths);
+                         d_tokens, d_lengths, 1);
       e = hipGetLastError();
       return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_forward launch");
     }
