@@ -593,7 +593,7 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru_kernel(const float* __res
 // wave, gh and the fp32 state through LDS, 12 waves -- issued ~2.6x the
 // instructions per step and needed two barriers.)
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-constexpr int kH16P = kH + 4;   // LDS pitch (halves) of the fp16 state image [batch][unit]
+constexpr int kH16P = kH + 8;   // LDS pitch (halves) of the fp16 state image [batch][unit]: 16-byte rows, conflict-free B reads
 constexpr int kGru16Waves = kH / 16, kGru16Threads = 64 * kGru16Waves;
 #ifndef WK_GRU_PF
 #define WK_GRU_PF 3
@@ -649,7 +649,18 @@ __global__ __launch_bounds__(kGru16Threads) void ctc_gru16_kernel(const __half* 
   const int64_t dstep = dir == 0 ? B : -B;
   const int64_t row = (int64_t)(dir == 0 ? 0 : T - 1) * B + (live ? b : 0);
   const __half* gq = gi + row * (6 * kH) + dir * 3 * kH + u0;
-  __half* oq = out + row * (2 * kH) + dir * kH + u0;
+  // Outputs: the new fp16 state of a step is already the [16 rows][128 units]
+  // image h16[cur] after the step's barrier; in the next step threads 0-255
+  // copy it out as one 16-byte load + store each (a row's 256 bytes by 16
+  // lanes) instead of every lane storing 8 bytes (32-byte pieces per row).
+  const int yn = (tid >> 4) & 15, yc = tid & 15;
+  const bool ylive = tid < 256 && (int64_t)blockIdx.x * kGruBatch + yn < B;
+  __half* yq = out + ((int64_t)(dir == 0 ? 0 : T - 1) * B + (ylive ? (int64_t)blockIdx.x * kGruBatch + yn : 0)) * (2 * kH) +
+               dir * kH + 8 * yc;
+  auto store_y = [&](int buf) {
+    if (ylive) *reinterpret_cast<uint4*>(yq) = *reinterpret_cast<const uint4*>(&h16[buf][yn * kH16P + 8 * yc]);
+    yq += dstep * (2 * kH);
+  };
   uint2 g_r[kGruPf], g_z[kGruPf], g_c[kGruPf];
   auto load_gates = [&](int j, int step) {   // gate inputs of `step` into ring slot j, then advance
     g_r[j] = *reinterpret_cast<const uint2*>(gq);
@@ -679,6 +690,7 @@ __global__ __launch_bounds__(kGru16Threads) void ctc_gru16_kernel(const __half* 
         an = __builtin_amdgcn_mfma_f32_16x16x16f16(wn[s], hv[s], an, 0, 0, 0);
       }
     }
+    if (step > 0) store_y(cur);   // the previous step's outputs
     const h4 gr = __builtin_bit_cast(h4, g_r[j]), gz = __builtin_bit_cast(h4, g_z[j]), gc = __builtin_bit_cast(h4, g_c[j]);
 #if WK_GRU_ABL != 2
     load_gates(j, step + kGruPf);
@@ -702,15 +714,12 @@ __global__ __launch_bounds__(kGru16Threads) void ctc_gru16_kernel(const __half* 
       h[i] = hn;
       o[i] = (_Float16)hn;
     }
-#if WK_GRU_ABL != 3
-    if (live) *reinterpret_cast<uint2*>(oq) = __builtin_bit_cast(uint2, o);
-#endif
-    oq += dstep * (2 * kH);
     *reinterpret_cast<uint2*>(&h16[cur ^ 1][n * kH16P + u0]) = __builtin_bit_cast(uint2, o);
     cur ^= 1;
     __syncthreads();
   }
   }
+  store_y(cur);   // the last step's outputs
 }
 
 // ---------------------------------------------------------------------------
