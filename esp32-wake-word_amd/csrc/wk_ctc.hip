@@ -595,19 +595,21 @@ __global__ __launch_bounds__(kGruThreads) void ctc_gru_kernel(const float* __res
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 constexpr int kH16P = kH + 8;   // LDS pitch (halves) of the fp16 state image [batch][unit]: 16-byte rows, conflict-free B reads
 constexpr int kGru16Waves = kH / 16, kGru16Threads = 64 * kGru16Waves;
+constexpr int kGtP = 3 * kH + 8;   // LDS pitch (halves) of a gate-input tile row: 16-byte aligned
 #ifndef WK_GRU_PF
-#define WK_GRU_PF 3
+#define WK_GRU_PF 2
 #endif
 constexpr int kGruPf = WK_GRU_PF;
 #ifndef WK_GRU_ABL
 #define WK_GRU_ABL 0
 #endif   // gate-input prefetch depth (steps)
 
-__global__ __launch_bounds__(kGru16Threads) void ctc_gru16_kernel(const __half* __restrict__ gi, const h4* __restrict__ whh_pk,
+__global__ __launch_bounds__(kGru16Threads, 4) void ctc_gru16_kernel(const __half* __restrict__ gi, const h4* __restrict__ whh_pk,
                                                                   const float* __restrict__ bih,
                                                                   const float* __restrict__ bhh, int64_t B, int T,
                                                                   __half* __restrict__ out) {   // fp16: the next GEMM's operand
   __shared__ __attribute__((aligned(16))) _Float16 h16[2][kGruBatch * kH16P];
+  __shared__ __attribute__((aligned(16))) _Float16 gt[2][kGruBatch * kGtP];   // gate-input tiles
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int dir = blockIdx.y;
@@ -638,17 +640,33 @@ __global__ __launch_bounds__(kGru16Threads) void ctc_gru16_kernel(const __half* 
     bh_c[i] = bh[2 * kH + u];
     h[i] = 0.0f;
   }
-  // Running pointers at the current step's row (a step moves them by one
-  // frame, +-768 / +-256 halfs).  A row's three gate inputs for the lane's 4
-  // units are three 8-byte loads, issued kGruPf steps ahead into a ring of
-  // registers (one step ahead left every step waiting on the load latency).
-  // The loads are unconditional -- idle lanes read utterance 0, and past the
-  // last step the pointer stays on the last row -- so no branch splits the
-  // load counter's view of the ring.
-  // gi and out are time-major (row t B + b): a step moves by B rows.
-  const int64_t dstep = dir == 0 ? B : -B;
-  const int64_t row = (int64_t)(dir == 0 ? 0 : T - 1) * B + (live ? b : 0);
-  const __half* gq = gi + row * (6 * kH) + dir * 3 * kH + u0;
+  // Gate inputs: a step's [16 rows][384] fp16 block of gi (this direction's
+  // half of 16 adjacent time-major rows) is loaded cooperatively, 16 bytes per
+  // thread and two chunks per thread (chunks past the 768 read out of range),
+  // kGruPf steps ahead into a register ring, written to an LDS tile one step
+  // ahead, and read back per lane (3 x 8 bytes).  The buffer resource is the
+  // step's block itself: rows past B fall outside num_records and read 0, the
+  // step index is clamped, so every load is unconditional and there is no
+  // per-lane branch.  (Per-lane 8-byte loads from gi -- 32-byte pieces per
+  // row and wave -- were the recurrence's largest cost.)
+  const int64_t b0 = (int64_t)blockIdx.x * kGruBatch;
+  const int nrow = (int)(B - b0 < kGruBatch ? B - b0 : kGruBatch);
+  const int gc0 = tid, gc1 = tid + kGru16Threads;   // 16-byte chunks: row c / 48, column c % 48
+  const int gvo0 = (gc0 / 48) * (12 * kH) + dir * (6 * kH) + (gc0 % 48) * 16;
+  const int gvo1 = gc1 < 16 * 48 ? (gc1 / 48) * (12 * kH) + dir * (6 * kH) + (gc1 % 48) * 16 : 0x40000000;
+  uint4 gv0[kGruPf], gv1[kGruPf];
+  auto load_gates = [&](int slot, int step) {
+    const int st = step < T ? step : T - 1;
+    const int t = dir == 0 ? st : T - 1 - st;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(gi + ((int64_t)t * B + b0) * (6 * kH), (uint32_t)nrow * (12 * kH));
+    gv0[slot] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, gvo0, 0, 0));
+    gv1[slot] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, gvo1, 0, 0));
+  };
+  auto stage_gates = [&](int slot, int buf) {   // ring slot -> LDS tile
+    *reinterpret_cast<uint4*>(&gt[buf][(gc0 / 48) * kGtP + (gc0 % 48) * 8]) = gv0[slot];
+    if (gc1 < 16 * 48) *reinterpret_cast<uint4*>(&gt[buf][(gc1 / 48) * kGtP + (gc1 % 48) * 8]) = gv1[slot];
+  };
+  const int64_t dstep = dir == 0 ? B : -B;   // out is time-major (row t B + b)
   // Outputs: the new fp16 state of a step is already the [16 rows][128 units]
   // image h16[cur] after the step's barrier; in the next step threads 0-255
   // copy it out as one 16-byte load + store each (a row's 256 bytes by 16
@@ -661,15 +679,10 @@ __global__ __launch_bounds__(kGru16Threads) void ctc_gru16_kernel(const __half* 
     if (ylive) *reinterpret_cast<uint4*>(yq) = *reinterpret_cast<const uint4*>(&h16[buf][yn * kH16P + 8 * yc]);
     yq += dstep * (2 * kH);
   };
-  uint2 g_r[kGruPf], g_z[kGruPf], g_c[kGruPf];
-  auto load_gates = [&](int j, int step) {   // gate inputs of `step` into ring slot j, then advance
-    g_r[j] = *reinterpret_cast<const uint2*>(gq);
-    g_z[j] = *reinterpret_cast<const uint2*>(gq + kH);
-    g_c[j] = *reinterpret_cast<const uint2*>(gq + 2 * kH);
-    gq += step + 1 < T ? dstep * (6 * kH) : 0;
-  };
 #pragma unroll
   for (int j = 0; j < kGruPf; ++j) load_gates(j, j);
+  stage_gates(0, 0);
+  load_gates(0, kGruPf);
   __syncthreads();
   int cur = 0;
   for (int step0 = 0; step0 < T; step0 += kGruPf) {
@@ -691,9 +704,13 @@ __global__ __launch_bounds__(kGru16Threads) void ctc_gru16_kernel(const __half* 
       }
     }
     if (step > 0) store_y(cur);   // the previous step's outputs
-    const h4 gr = __builtin_bit_cast(h4, g_r[j]), gz = __builtin_bit_cast(h4, g_z[j]), gc = __builtin_bit_cast(h4, g_c[j]);
+    const _Float16* gp = &gt[step & 1][n * kGtP + u0];
+    const h4 gr = *reinterpret_cast<const h4*>(gp), gz = *reinterpret_cast<const h4*>(gp + kH),
+             gc = *reinterpret_cast<const h4*>(gp + 2 * kH);
+    // next step's gates into the other tile, then refill that ring slot
+    stage_gates((j + 1) % kGruPf, (step + 1) & 1);
 #if WK_GRU_ABL != 2
-    load_gates(j, step + kGruPf);
+    load_gates((j + 1) % kGruPf, step + 1 + kGruPf);
 #endif
     h4 o;
 #pragma unroll
