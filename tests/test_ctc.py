@@ -165,6 +165,27 @@ def test_ctc_bit_repeatable_at_scale(precision):
 
 
 @pytest.mark.gpu
+def test_ctc_fp16_tail_launch_matches_chunked():
+    """fp16 argmax-only decode of 400 utterances (120,400 time-major rows: on a
+    256-CU device the output layer runs as 256 x 384-row blocks plus a tail
+    launch with 2 row tiles per wave) gives the same tokens and lengths as four
+    100-utterance batches (one launch each)."""
+    import wakeword
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    m = CO.make_model(V, seed=5)
+    g = wakeword.CTCModel(CO.flat_weights(m), V, precision="fp16")
+    audio = wakeword.synth_clips(91, 0, 400, 48000)
+    feats = g.features(audio, n_samples=48000)
+    tok, ln, _ = g.decode(feats)
+    tok, ln = tok.clone(), ln.clone()
+    for i in range(4):
+        t4, l4, _ = g.decode(feats[100 * i:100 * (i + 1)].contiguous())
+        assert torch.equal(l4, ln[100 * i:100 * (i + 1)])
+        assert torch.equal(t4, tok[100 * i:100 * (i + 1)])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("precision", ["fp32", "fp16"])
 def test_ctc_long_utterance_and_device_decode(ctc, precision):
     """8 s utterances (T = 801, Config.max_audio_length): the z-score's
