@@ -956,15 +956,13 @@ constexpr int out_rf(bool logits) { return logits ? 2 : kOutRF; }
 constexpr int out_rows(bool logits) { return 16 * out_rf(logits) * kOutWaves; }
 static_assert(kOutPre * 64 * kOutWaves == kOutBN * (kOutK / 8), "W tile chunks divide over the threads");
 
-// RF_ > 0 overrides the row tiles per wave (the tail launch, below); blocks
-// start at row row_begin.
-template <bool LOGITS, int RF_ = 0>
+template <bool LOGITS>
 __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const __half* __restrict__ y,
                                                                           const __half* __restrict__ w,
                                                                           const float* __restrict__ bias, int64_t rows,
                                                                           int V, __half* __restrict__ logits,
-                                                                          int* __restrict__ best, int64_t row_begin) {
-  constexpr int kOutRF = RF_ > 0 ? RF_ : out_rf(LOGITS), kOutRows = 16 * kOutRF * kOutWaves;
+                                                                          int* __restrict__ best) {
+  constexpr int kOutRF = out_rf(LOGITS), kOutRows = out_rows(LOGITS);
   __shared__ __attribute__((aligned(16))) _Float16 bt[2][kOutBN * kOutPitch];
   // the tile's bias, staged with its W rows (an L2 load per column in the
   // epilogue stalled it); replicated x4 so one ds_read_b128 is an MFMA C operand
@@ -972,7 +970,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const bool wave0 = __builtin_amdgcn_readfirstlane(wv) == 0;
-  const int64_t row0 = row_begin + (int64_t)blockIdx.x * kOutRows + 16 * kOutRF * wv;
+  const int64_t row0 = (int64_t)blockIdx.x * kOutRows + 16 * kOutRF * wv;
   // A fragments: rows row0 + 16 rf + li, k = 32 s + 8 lg .. +7
   h8 a[kOutRF][8];
 #pragma unroll
@@ -1430,26 +1428,12 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
       const dim3 og((unsigned)((rows + out_rows(d_log_probs != nullptr) - 1) / out_rows(d_log_probs != nullptr)));
       if (d_log_probs) {
         hipLaunchKernelGGL(ctc_out_argmax16_kernel<true>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
-                           c->out_b, rows, V, c->logits16, c->best, (int64_t)0);
+                           c->out_b, rows, V, c->logits16, c->best);
         hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits16,
                            c->out_b, rows, V, d_log_probs, (int*)nullptr, (int)batch, T);
       } else {
-        // One workgroup per CU (244 VGPRs): the launch runs in waves of n_cu
-        // blocks.  When the last wave would be less than 2/3 full, the rows
-        // after the full waves go to a second launch with 2 row tiles per wave
-        // (2/3 of a block's MFMA work), which fits in one wave of blocks.
-        constexpr int rows3 = out_rows(false), rows2 = 16 * 2 * kOutWaves;
-        const int64_t nb3 = (rows + rows3 - 1) / rows3, full = nb3 / c->n_cu * c->n_cu;
-        const int64_t head = full * rows3 < rows ? full * rows3 : rows, tail = rows - head;
-        const bool split = kOutRF == 3 && tail > 0 && full > 0 && (tail + rows2 - 1) / rows2 <= c->n_cu;
-        const int64_t main_rows = split ? head : rows;
-        hipLaunchKernelGGL(ctc_out_argmax16_kernel<false>, dim3((unsigned)((main_rows + rows3 - 1) / rows3)),
-                           dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, (__half*)nullptr, c->best,
-                           (int64_t)0);
-        if (split)
-          hipLaunchKernelGGL((ctc_out_argmax16_kernel<false, 2>), dim3((unsigned)((tail + rows2 - 1) / rows2)),
-                             dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, (__half*)nullptr,
-                             c->best, head);
+        hipLaunchKernelGGL(ctc_out_argmax16_kernel<false>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
+                           c->out_b, rows, V, (__half*)nullptr, c->best);
       }
       hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
                          d_tokens, d_lengths, 1);
