@@ -630,16 +630,18 @@ __global__ __launch_bounds__(kGru16Threads, 4) void ctc_gru16_kernel(const __hal
   for (int i = tid; i < kGruBatch * kH16P; i += kGru16Threads) h16[0][i] = (_Float16)0.0f;
   const float* bi = bih + dir * 3 * kH;
   const float* bh = bhh + dir * 3 * kH;
-  float b_r[4], b_z[4], bi_c[4], bh_c[4], h[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int u = u0 + i;
-    b_r[i] = bi[u] + bh[u];
-    b_z[i] = bi[kH + u] + bh[kH + u];
-    bi_c[i] = bi[2 * kH + u];
-    bh_c[i] = bh[2 * kH + u];
-    h[i] = 0.0f;
+  // Biases in LDS, [gate term][unit] (b_ir + b_hr, b_iz + b_hz, b_in, b_hn):
+  // read per step as four 16-byte loads (in VGPRs they pushed the kernel over
+  // the 128 registers of 4 waves per SIMD).
+  __shared__ f32x4 gbias[4][kH / 4];
+  if (tid < kH) {
+    float* gbf = reinterpret_cast<float*>(&gbias[0][0]);
+    gbf[tid] = bi[tid] + bh[tid];
+    gbf[kH + tid] = bi[kH + tid] + bh[kH + tid];
+    gbf[2 * kH + tid] = bi[2 * kH + tid];
+    gbf[3 * kH + tid] = bh[2 * kH + tid];
   }
+  float h[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   // Gate inputs: a step's [16 rows][384] fp16 block of gi (this direction's
   // half of 16 adjacent time-major rows) is loaded cooperatively, 16 bytes per
   // thread and two chunks per thread (chunks past the 768 read out of range),
@@ -712,6 +714,9 @@ __global__ __launch_bounds__(kGru16Threads, 4) void ctc_gru16_kernel(const __hal
 #if WK_GRU_ABL != 2
     load_gates((j + 1) % kGruPf, step + 1 + kGruPf);
 #endif
+    int bq = u0 >> 2;
+    asm volatile("" : "+v"(bq));   // re-read per step, not hoisted into 16 VGPRs
+    const f32x4 b_r = gbias[0][bq], b_z = gbias[1][bq], bi_c = gbias[2][bq], bh_c = gbias[3][bq];
     h4 o;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
