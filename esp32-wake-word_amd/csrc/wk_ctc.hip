@@ -224,18 +224,28 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
       if (q == 0) pw[200] = __builtin_fmaf(v[10].x, v[10].x, v[10].y * v[10].y);
     }
     wave_lds_sync();
-    // power -> HTK mel (CSR) -> ln(+1e-8): task (frame, mel) over the wave's lanes
-    for (int i = lane; i < kFftFrames * kMels; i += 64) {
-      const int ff = i / kMels, m = i - kMels * (i / kMels);
-      const int64_t r = ps * kFftFrames + ff;
-      if (r < rows) {
-        const int s0 = L.fbs[m], n = L.fbl[m], o = L.fbo[m];
-        const float* pw = PW + ff * kPwPitch + s0;
-        float acc = 0.0f;
-        for (int j = 0; j < n; ++j) acc = __builtin_fmaf(pw[j], L.fbw[o + j], acc);
-        feats[r * kMels + m] = wk_logf(acc + 1e-8f);
+    // power -> HTK mel (CSR) -> ln(+1e-8): lane = mel, all three frames per
+    // weight (lanes 0-15 also take mel 64 + lane).  A wave walks the widest
+    // filter of each of the two lane sets (~9 + 12 taps) instead of four rounds
+    // of (frame, mel) tasks, each as long as its widest filter (~44 taps).
+    auto mel3 = [&](int m) {
+      const int s0 = L.fbs[m], n = L.fbl[m], o = L.fbo[m];
+      const float* pw = PW + s0;
+      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+      for (int j = 0; j < n; ++j) {
+        const float wj = L.fbw[o + j];
+        a0 = __builtin_fmaf(pw[j], wj, a0);
+        a1 = __builtin_fmaf(pw[kPwPitch + j], wj, a1);
+        a2 = __builtin_fmaf(pw[2 * kPwPitch + j], wj, a2);
       }
-    }
+      const int64_t r0 = ps * kFftFrames;
+      if (r0 < rows) feats[r0 * kMels + m] = wk_logf(a0 + 1e-8f);
+      if (r0 + 1 < rows) feats[(r0 + 1) * kMels + m] = wk_logf(a1 + 1e-8f);
+      if (r0 + 2 < rows) feats[(r0 + 2) * kMels + m] = wk_logf(a2 + 1e-8f);
+    };
+    static_assert(kFftFrames == 3 && kMels > 64 && kMels <= 128, "mel lane mapping");
+    mel3(lane);
+    if (lane < kMels - 64) mel3(64 + lane);
     wave_lds_sync();
   }
 }
