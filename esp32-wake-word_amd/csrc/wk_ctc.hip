@@ -688,7 +688,9 @@ __global__ __launch_bounds__(kGru16Threads, 4) void ctc_gru16_kernel(const __hal
   __half* yq = out + ((int64_t)(dir == 0 ? 0 : T - 1) * B + (ylive ? (int64_t)blockIdx.x * kGruBatch + yn : 0)) * (2 * kH) +
                dir * kH + 8 * yc;
   auto store_y = [&](int buf) {
+#if WK_GRU_ABL != 3
     if (ylive) *reinterpret_cast<uint4*>(yq) = *reinterpret_cast<const uint4*>(&h16[buf][yn * kH16P + 8 * yc]);
+#endif
     yq += dstep * (2 * kH);
   };
 #pragma unroll
