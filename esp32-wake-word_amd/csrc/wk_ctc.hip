@@ -952,6 +952,9 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef WK_OUT_SKEW
 #define WK_OUT_SKEW 1
 #endif
+#ifndef WK_OUT_DMA
+#define WK_OUT_DMA 1
+#endif
 #ifndef WK_OUT_PRIO
 #define WK_OUT_PRIO 0
 #endif
@@ -1005,8 +1008,35 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   // loads: rows past V come back 0 from the range check, no branch per load.
   const __amdgpu_buffer_rsrc_t wrs = make_rsrc(w, (uint32_t)V * kOutK * 2);
   const __amdgpu_buffer_rsrc_t brs = make_rsrc(bias, (uint32_t)V * 4);
-  uint4 pre[kOutPre];
   float pb = 0.0f;
+#if WK_OUT_DMA
+  // W tile nt -> bt[nt & 1] by LDS-DMA (buffer_load ... lds), issued by waves
+  // 0-3 after their MFMA phase: instruction i of wave w fills 1 KB = rows
+  // 2 (8 w + i) and +1; lane L writes position L & 31 of its row, so it loads
+  // global chunk (L & 31) ^ (row & 15) -- the swizzle is in the global
+  // addresses.  The compiler makes every LDS read after an LDS-DMA wait for
+  // it, so no wave issues one before its own B-fragment reads of the period;
+  // the target buffer was last read in the previous period, and the explicit
+  // vmcnt(0) before the closing barrier completes the DMA.
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  constexpr int kDmaWaves = kOutWaves / 2, kDmaPer = kOutBN * kOutK * 2 / 1024 / kDmaWaves;
+  auto dma_w = [&](int nt) {
+    if (wvu >= kDmaWaves) return;
+#pragma unroll
+    for (int i = 0; i < kDmaPer; ++i) {
+      const int q = wvu * kDmaPer + i, rr = 2 * q + (lane >> 5), c = (lane & 31) ^ (rr & 15);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)&bt[nt & 1][q * 512], 16,
+                                               (nt * kOutBN + rr) * (kOutK * 2) + 16 * c, 0, 0, 0);
+    }
+  };
+  auto fetch = [&](int nt) {   // the tile's bias (W comes by dma_w)
+    if (wave0) pb = buf_load(brs, 4 * (nt * kOutBN + tid), 0);
+  };
+  auto stash = [&](int buf) {
+    if (wave0) bsh[buf][tid] = f32x4{pb, pb, pb, pb};
+  };
+#else
+  uint4 pre[kOutPre];
   auto fetch = [&](int nt) {
 #pragma unroll
     for (int i = 0; i < kOutPre; ++i) {
@@ -1024,8 +1054,13 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     }
     if (wave0) bsh[buf][tid] = f32x4{pb, pb, pb, pb};
   };
+#endif
   fetch(0);
   stash(0);
+#if WK_OUT_DMA
+  dma_w(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   __syncthreads();
   float mx[kOutRF][4];
   int ix[kOutRF][4];
@@ -1101,13 +1136,23 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
             acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf[cf], acc[rf][cf], 0, 0, 0);
       }
     }
+#if WK_OUT_DMA
+    if (!lag && nt + 1 < NT) {   // after this wave's last LDS read of the period
+      stash((nt + 1) & 1);
+      dma_w(nt + 1);
+    }
+#endif
     if (!lag) {
       epilogue(nt, bbc);
     } else if (!kBiasAcc) {
 #pragma unroll
       for (int cf = 0; cf < 4; ++cf) bprev[cf] = bbc[cf];
     }
+#if WK_OUT_DMA
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // LDS-DMA done (the barrier's own wait omits it)
+#else
     if (nt + 1 < NT) stash((nt + 1) & 1);
+#endif
     __syncthreads();
   }
   if (lag && NT > 0) epilogue(NT - 1, bprev);
