@@ -212,3 +212,54 @@ def test_ctc_long_utterance_and_device_decode(ctc, precision):
         ref_lp = m(ref_f)
     assert np.abs((lp - ref_lp).numpy()).max() <= (LOGP_ATOL if precision == "fp32" else 0.05)
     assert seqs == g.forward(feats)   # the argmax-only kernel agrees with the log-prob path
+
+
+def test_ctc_state_dict_bound_by_name():
+    """CTCModel binds a GRU_CTC_Model state dict by key (ctc.py:119-146), in any
+    order; missing, unexpected or mis-shaped keys are rejected (host-only)."""
+    import random
+    from wakeword.ctc import ctc_state_dict_spec, pack_state_dict
+    m = CO.make_model(37, seed=2)
+    sd = m.state_dict()
+    assert [k for k, _ in ctc_state_dict_spec(37)] == list(sd.keys())
+    assert [s for _, s in ctc_state_dict_spec(37)] == [tuple(v.shape) for v in sd.values()]
+    keys = list(sd.keys())
+    random.Random(0).shuffle(keys)
+    shuffled = {k: sd[k] for k in keys}
+    assert np.array_equal(pack_state_dict(shuffled, 37), CO.flat_weights(m))
+    with pytest.raises(ValueError, match="missing"):
+        pack_state_dict({k: v for k, v in sd.items() if k != "gru.bias_hh_l1"}, 37)
+    with pytest.raises(ValueError, match="unexpected"):
+        pack_state_dict({**sd, "gru.weight_ih_l2": sd["gru.weight_ih_l1"]}, 37)
+    bad = dict(sd)
+    bad["gru.weight_hh_l0"], bad["gru.weight_ih_l0"] = sd["gru.weight_ih_l0"].T, sd["gru.weight_hh_l0"]
+    assert bad["gru.weight_hh_l0"].shape == (128, 384)
+    with pytest.raises(ValueError, match="shape"):
+        pack_state_dict(bad, 37)
+    with pytest.raises(ValueError, match="shape"):
+        pack_state_dict(sd, 40)         # vocab disagrees with output_layer
+
+
+def test_ctc_decode_predictions_text_round_trip():
+    """decode_predictions (ctc.py:453-471): argmax, blank drop, repeat collapse,
+    idx_to_char with "<unk>" for unmapped ids -- text equals the oracle's token
+    ids mapped through the same vocabulary."""
+    from wakeword.ctc import decode_predictions, greedy_tokens, tokens_to_text
+    vocab = {"<blank>": 0, "<unk>": 1}
+    for ch in "你好小爱同学abc":
+        vocab[ch] = len(vocab)
+    idx_to_char = {i: c for c, i in vocab.items()}
+    text = "小爱同学你好"
+    ids = [vocab[c] for c in text]
+    frames = []
+    for i in ids:                               # each char for 2 frames, blank between
+        frames += [i, i, 0]
+    lp = torch.full((1, len(frames), len(vocab) + 3), -9.0)
+    for t, k in enumerate(frames):
+        lp[0, t, k] = 0.0
+    assert decode_predictions(lp, idx_to_char) == [text]
+    assert greedy_tokens(lp) == CO.greedy_decode(lp)
+    lp2 = torch.randn(4, 50, len(vocab) + 3, generator=torch.Generator().manual_seed(3))
+    seqs = CO.greedy_decode(lp2)
+    assert decode_predictions(lp2, idx_to_char) == tokens_to_text(seqs, idx_to_char)
+    assert any("<unk>" in s for s in decode_predictions(lp2, idx_to_char))   # ids past the map
