@@ -3,6 +3,15 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+Started without torchrun (WORLD_SIZE unset) and with --gpus N > 1, the
+process launches N ranks itself before touching the GPU: N fresh child
+processes of this script with torchrun's environment (RANK = LOCAL_RANK = i,
+WORLD_SIZE = N, MASTER_ADDR 127.0.0.1, a free MASTER_PORT), one GPU each, and
+exits with the first failing child's status.  Every rank checks its handle's
+device error word after the timed region (wk_check_device_errors, outside the
+timing); a flag on any rank means a role hand-off aborted and the logits are
+invalid, and then no bench line is printed (exit status 3).
+
 One step = one pass of the hot path (1 s @ 16 kHz audio -> MFCC (torchaudio
 definition + CMVN) -> xiaoa CNN -> logit, fp32) over one batch of B synthetic
 clips that are already resident in HBM (B = 65,536 per
@@ -17,6 +26,8 @@ import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -80,6 +91,58 @@ def parse():
     return ap.parse_args()
 
 
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def rank_envs(n: int, port: int, base=None):
+    """torchrun's per-rank environment for n local ranks (one GPU each)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "GROUP_RANK": "0", "ROLE_RANK": str(r), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                  "TORCHELASTIC_RUN_ID": "bench"})
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL (the host driver's only mode)
+        envs.append(e)
+    return envs
+
+
+def spawn_ranks(argv, n: int, timeout: float = None) -> int:
+    """Run `argv` as n ranks (child processes, torchrun-style env) and wait.
+    Returns 0 if all ranks succeed, else the first failing rank's status (the
+    others are terminated).  Called before any GPU call in this process."""
+    procs = [subprocess.Popen(argv, env=e) for e in rank_envs(n, free_port())]
+    deadline = None if timeout is None else time.monotonic() + timeout
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                r = p.poll()
+                if r is None:
+                    continue
+                pending.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r if r > 0 else 128 - r
+                    for q in pending:
+                        q.terminate()
+            if deadline is not None and time.monotonic() > deadline and pending:
+                rc = rc or 124
+                for q in pending:
+                    q.kill()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def cpu_baseline(seconds: float):
     """The ml_models CPU path (torch fp32 restatement, oracle/wk_torch_cpu.py) on
     the host cores, timed on a bounded sample of the same synthetic workload."""
@@ -101,6 +164,7 @@ def cpu_baseline(seconds: float):
         if el >= seconds and n >= 4 * batch:
             break
     return {"value": round(n / el, 1), "unit": "windows/s", "cores": torch.get_num_threads(),
+            "host_cpus": len(os.sched_getaffinity(0)),
             "kind": "port",
             "sample": f"{n} windows = {n // batch} batches of {batch} synthetic clips (seed 1234), "
                       f"{el:.1f} s; torch-CPU fp32 restatement of the torchaudio MFCC+CMVN front-end "
@@ -120,6 +184,9 @@ def load_traffic(precision="fp32"):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # self-launch: N ranks before this process makes any GPU call
+        sys.exit(spawn_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
     import torch
     import torch.distributed as dist
     import wakeword
@@ -129,8 +196,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"# note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     ndev = torch.cuda.device_count()
     if args.dist_backend == "nccl" and local >= ndev:
         raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPU(s) visible")
@@ -146,6 +213,8 @@ def main():
     def barrier():
         if world > 1:
             dist.barrier()
+
+    pg_world = dist.get_world_size() if world > 1 else 1
 
     B = args.batch
     model = wakeword.load_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"), device=local,
@@ -185,12 +254,23 @@ def main():
     elapsed = time.perf_counter() - t0
     launch_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
 
-    t = torch.tensor([elapsed, launch_ms], dtype=torch.float64,
+    # outside the timed region: this rank's device error word (role hand-off
+    # aborts) and the logits' finiteness, reduced with the times
+    flags = C.c_uint32(0)
+    st_err = L.wk_check_device_errors(h, C.byref(flags))
+    bad = float(st_err != 0 or flags.value != 0 or not bool(torch.isfinite(logits).all()))
+    t = torch.tensor([elapsed, launch_ms, bad], dtype=torch.float64,
                      device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)   # the slowest rank's time
-    elapsed, launch_ms = float(t[0]), float(t[1])
-    finite = bool(torch.isfinite(logits).all())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)   # the slowest rank's time, any rank's error
+    elapsed, launch_ms, bad = float(t[0]), float(t[1]), float(t[2])
+    if bad:
+        if rank == 0:
+            print(f"bench: a rank reported a device error or non-finite logits (this rank: status {st_err}, "
+                  f"flags {flags.value:#x}); no measurement printed", file=sys.stderr)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(3)
 
     if rank == 0:
         total = world * B * args.steps
@@ -216,6 +296,7 @@ def main():
                        "audio": "fp32 samples" if args.audio == "f32" else "int16 PCM samples",
                        "batch_per_gpu": B, "global_batch": world * B, "seq_len": 16000,
                        "parallelism": f"dp{world} (per-rank clip split, no collectives)",
+                       "process_group_world_size": pg_world,
                        **({"dist_backend": args.dist_backend} if world > 1 else {})},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1),
                          "peak_basis": peak_basis,
@@ -225,7 +306,8 @@ def main():
                          "flop_per_window": FLOP_PER_WINDOW,
                          "hbm_gbs_algorithmic": round((BYTES_PER_WINDOW_F32 if args.audio == "f32" else 32_004) * B
                                                       / (launch_ms * 1e-3) / 1e9, 1)},
-            "logits_finite": finite,
+            "logits_finite": True,
+            "device_errors": 0,
         }
         if traffic_src:
             out["roofline"]["traffic_source"] = traffic_src

@@ -234,7 +234,7 @@ wk_status wk_cnn(wk_handle* h, const float* d_feats, int64_t batch, float* d_log
     hipError_t e = h->cfg.precision == WK_PREC_INT8
                        ? wk::launch_int8_cnn(d_feats, batch, h->d_int8, d_logits, 4 * h->n_cu, (hipStream_t)stream)
                        : wk::launch_cnn_fused(d_feats, batch, h->d_packed, h->d_bf16, conv_mode_of(h), d_logits, h->n_cu,
-                                              (hipStream_t)stream);
+                                              (hipStream_t)stream, h->d_err);
     return e == hipSuccess ? WK_OK : hip_fail(e, "cnn launch");
   });
 }
@@ -276,7 +276,7 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
       if (e != hipSuccess) return hip_fail(e, "frontend launch");
       e = int8 ? wk::launch_int8_cnn(feats, n, h->d_int8, d_logits + c0, 4 * h->n_cu, (hipStream_t)stream)
                : wk::launch_cnn_fused(feats, n, h->d_packed, h->d_bf16, conv_mode_of(h), d_logits + c0, h->n_cu,
-                                      (hipStream_t)stream);
+                                      (hipStream_t)stream, h->d_err);
       if (e != hipSuccess) return hip_fail(e, "cnn launch");
     }
     if (ws_lock.owns_lock()) {

@@ -903,6 +903,16 @@ __global__ __launch_bounds__(256) void ctc_argmax_only_kernel(const LT* __restri
 // (One thread per utterance walking its T frames serially took 0.17 ms per
 // 4096 utterances: strided, dependent loads.)
 // tm: best is time-major (frame t of utterance b at t B + b).
+// decode_predictions' per-frame argmax (ctc.py:454) in batch-major order:
+// pred[b][t] from the output layer's best[] (time-major rows in fp16 mode).
+__global__ __launch_bounds__(256) void ctc_pred_kernel(const int* __restrict__ best, int64_t B, int T, int tm,
+                                                       int* __restrict__ pred) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= B * (int64_t)T) return;
+  const int64_t b = r / T, t = r - b * T;
+  pred[r] = best[tm ? t * B + b : r];
+}
+
 __global__ __launch_bounds__(256) void ctc_greedy_kernel(const int* __restrict__ best, int64_t B, int T,
                                                          int* __restrict__ tokens, int* __restrict__ lengths,
                                                          int tm = 0) {
@@ -938,9 +948,10 @@ __global__ __launch_bounds__(256) void ctc_greedy_kernel(const int* __restrict__
 // B-fragment ds_read_b128 is conflict-free), one barrier per tile.  Each lane keeps
 // a running (max, index) for its 4 RF rows over its columns, visited in increasing
 // order, then 16-lane shuffles pick the first maximum (torch.max semantics).
-// LOGITS = true also stores fp16 logits for the log_softmax kernel; the argmax
-// is this kernel's in both cases, so tokens do not depend on log-probs being
-// requested.
+// LOGITS = true also stores the fp16 logits (bias included) for the log_softmax
+// kernel; the argmax is this kernel's in both cases and both variants
+// accumulate identically (bias as the first MFMA's C operand, the same K
+// order), so tokens do not depend on log-probs being requested.
 // ---------------------------------------------------------------------------
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef WK_OUT_RF
@@ -1076,13 +1087,10 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   // VALU beside its partner's MFMAs instead of both SIMD waves alternating
   // all-MFMA and all-VALU phases in step.
   const bool lag = WK_OUT_SKEW && __builtin_amdgcn_readfirstlane(wv) >= kOutWaves / 2;
-  // Argmax-only: the bias is the MFMAs' initial C operand (one ds_read_b128 of
-  // the replicated bias per column tile), so the epilogue is compare + select.
-  // LOGITS stores the bias-free logits (log_softmax adds it) and adds it here.
-  constexpr bool kBiasAcc = !LOGITS;
+  // The bias is the MFMAs' initial C operand (one ds_read_b128 of the
+  // replicated bias per column tile), so the epilogue is compare + select.
   f32x4 acc[kOutRF][4];
-  float bprev[4];
-  auto epilogue = [&](int tile, const float* bb4) {
+  auto epilogue = [&](int tile) {
     // column v = 64 tile + 16 cf + li, rows row0 + 16 rf + 4 lg + i
 #pragma unroll
     for (int cf = 0; cf < 4; ++cf) {
@@ -1092,7 +1100,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
         for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float z = kBiasAcc ? acc[rf][cf][i] : acc[rf][cf][i] + bb4[cf];
+            const float z = acc[rf][cf][i];
             if (z > mx[rf][i]) { mx[rf][i] = z; ix[rf][i] = v; }
             if (LOGITS) {
               const int64_t r = row0 + 16 * rf + 4 * lg + i;
@@ -1108,12 +1116,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   for (int nt = 0; nt < NT; ++nt) {
     if (nt + 1 < NT) fetch(nt + 1);
     const _Float16* b = bt[nt & 1];
-    float bbc[4];   // LOGITS: the tile's bias for the epilogue add
-    if (!kBiasAcc) {
-#pragma unroll
-      for (int cf = 0; cf < 4; ++cf) bbc[cf] = bsh[nt & 1][16 * cf + li][0];
-    }
-    if (lag && nt > 0) epilogue(nt - 1, bprev);
+    if (lag && nt > 0) epilogue(nt - 1);
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       h8 bf[4];
@@ -1123,7 +1126,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       if (st == 0) {
 #pragma unroll
         for (int cf = 0; cf < 4; ++cf) {
-          const f32x4 c0 = kBiasAcc ? bsh[nt & 1][16 * cf + li] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          const f32x4 c0 = bsh[nt & 1][16 * cf + li];
 #pragma unroll
           for (int rf = 0; rf < kOutRF; ++rf)
             acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][0], bf[cf], c0, 0, 0, 0);
@@ -1142,12 +1145,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       dma_w(nt + 1);
     }
 #endif
-    if (!lag) {
-      epilogue(nt, bbc);
-    } else if (!kBiasAcc) {
-#pragma unroll
-      for (int cf = 0; cf < 4; ++cf) bprev[cf] = bbc[cf];
-    }
+    if (!lag) epilogue(nt);
 #if WK_OUT_DMA
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // LDS-DMA done (the barrier's own wait omits it)
 #else
@@ -1155,7 +1153,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #endif
     __syncthreads();
   }
-  if (lag && NT > 0) epilogue(NT - 1, bprev);
+  if (lag && NT > 0) epilogue(NT - 1);
   // first maximum across the 16 column lanes of each row
 #pragma unroll
   for (int rf = 0; rf < kOutRF; ++rf)
@@ -1210,6 +1208,7 @@ struct wk_ctc {
   float* bhh[2];        // per layer: [768]
   float* whh_pk[2];     // per layer: [2 dir][24 tiles][32 k-steps][64 lanes]
   float *out_w, *out_b; // [V][256], [V]
+  float* zero_b;        // [V] zeros: the log_softmax kernel's bias in fp16 mode (the logits carry theirs)
   __half* wih16[2];     // fp16 copies (precision 1)
   __half* whh16_pk[2];  // per layer: [2 dir][24 tiles][8 k-steps][64 lanes][4]
   __half* out_w16;
@@ -1223,6 +1222,8 @@ struct wk_ctc {
   float *x0, *gi, *y0, *y1, *logits;
   __half *x0h, *y0h, *y1h, *logits16;
   int* best;
+  int64_t last_batch;   // geometry of the last wk_ctc_forward (wk_ctc_frame_argmax)
+  int32_t last_T;
 };
 
 namespace {
@@ -1246,7 +1247,7 @@ void free_ws(wk_ctc* c) {
 void free_all(wk_ctc* c) {
   free_ws(c);
   void* ps[] = {c->enc_w, c->enc_b, c->ln_g, c->ln_b, c->wih[0], c->wih[1], c->bih[0], c->bih[1], c->bhh[0],
-                c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->fb_w, c->wih16[0], c->wih16[1],
+                c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->zero_b, c->fb_w, c->wih16[0], c->wih16[1],
                 c->out_w16, c->fft_win, c->fft_tw, c->fb_start, c->fb_len, c->fb_off, c->whh16_pk[0], c->whh16_pk[1]};
   for (void* q : ps) (void)hipFree(q);
   if (c->blas) rocblas_destroy_handle(c->blas);
@@ -1347,6 +1348,10 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     if (e == hipSuccess) e = upload(&c->out_w, ow, (size_t)V * 2 * H);
     if (e == hipSuccess && c->f16) e = upload_f16(&c->out_w16, ow, (size_t)V * 2 * H);
     if (e == hipSuccess) e = upload(&c->out_b, take(V), V);
+    if (e == hipSuccess) {
+      const std::vector<float> z((size_t)V, 0.0f);
+      e = upload(&c->zero_b, z.data(), (size_t)V);
+    }
     // FFT tables: periodic Hann(400) and the four-step twiddles W400^(n2 k1), in double -> fp32
     {
       std::vector<float> wnd(kNfft), tw(2 * 400);
@@ -1459,6 +1464,8 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
       c->ws_rows = rows;
     }
     if (rocblas_set_stream(c->blas, st) != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_set_stream");
+    c->last_batch = batch;
+    c->last_T = T;
     const int enc_grid = (int)((rows + 63) / 64 < 8 * c->n_cu ? (rows + 63) / 64 : 8 * c->n_cu);
     if (f16)
       hipLaunchKernelGGL(ctc_encoder16_kernel, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w, c->enc_b,
@@ -1492,7 +1499,7 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
         hipLaunchKernelGGL(ctc_out_argmax16_kernel<true>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
                            c->out_b, rows, V, c->logits16, c->best);
         hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits16,
-                           c->out_b, rows, V, d_log_probs, (int*)nullptr, (int)batch, T);
+                           c->zero_b, rows, V, d_log_probs, (int*)nullptr, (int)batch, T);   // bias already in
       } else {
         hipLaunchKernelGGL(ctc_out_argmax16_kernel<false>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
                            c->out_b, rows, V, (__half*)nullptr, c->best);
@@ -1516,6 +1523,20 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
                        d_tokens, d_lengths);
     e = hipGetLastError();
     return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_forward launch");
+  });
+}
+
+wk_status wk_ctc_frame_argmax(wk_ctc* c, int64_t batch, int32_t T, int32_t* d_pred, void* stream) {
+  if (!c || batch < 0 || T < 1 || (batch > 0 && !d_pred)) return invalid("wk_ctc_frame_argmax: bad arguments");
+  if (batch == 0) return WK_OK;
+  if (batch != c->last_batch || T != c->last_T || !c->best)
+    return invalid("wk_ctc_frame_argmax: batch and T must be those of the handle's last wk_ctc_forward");
+  return on_device(c->cfg.device, [&]() -> wk_status {
+    const int64_t rows = batch * (int64_t)T;
+    hipLaunchKernelGGL(ctc_pred_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, (hipStream_t)stream, c->best,
+                       batch, T, c->f16 ? 1 : 0, d_pred);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_frame_argmax launch");
   });
 }
 

@@ -743,9 +743,16 @@ struct LogmelSrc {
     lane = lane_;
     signal_set(ctrl, kCtrlLFree + cw, cw < NBF ? (unsigned)cw : 0xFFFFFFFFu, lane);
   }
+  // A true answer is an acquire, like spin_until's exit: the compiler may not
+  // move the caller's reads of the log-mel buffer (load() below) above the
+  // ready-count read (LDS operations of a wave then complete in order).
   __device__ __forceinline__ bool ready(int64_t i) const {
-    return (exp_flags & 2) ||
-           __builtin_amdgcn_readfirstlane(lds_load(ctrl + kCtrlLReady)) >= 8u * (unsigned)(i + 1);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const bool r = (exp_flags & 2) ||
+                   __builtin_amdgcn_readfirstlane(lds_load(ctrl + kCtrlLReady)) >= 8u * (unsigned)(i + 1);
+    asm volatile("" ::: "memory");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    return r;
   }
   __device__ __forceinline__ void wait(int64_t i) const {
     if (!(exp_flags & 2)) spin_until<0>(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
@@ -761,6 +768,18 @@ struct LogmelSrc {
     signal_set(ctrl, kCtrlLFree + cw, (unsigned)(i + NBF), lane);
   }
 };
+
+// Protocol health: a spin that timed out set its role's abort word, and every
+// logit of the launch is then suspect.  Each wave reports what it sees on exit
+// to the handle's error word (host-visible; read by wk_check_device_errors /
+// wk_stream_push): bit 0 = a spin timed out, bit 1 = the abort word holds a
+// value no spin writes (LDS corruption).
+__device__ __forceinline__ void report_abort(const unsigned* ctrl, unsigned* err, int lane) {
+  if (lane == 0 && err) {
+    const unsigned ab = lds_load(ctrl + kCtrlAbort);
+    if (ab) __hip_atomic_store(err, ab == 1u ? 1u : 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 
 template <typename T, int CM, bool FEATS>
 __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __restrict__ audio, int64_t batch,
@@ -798,15 +817,7 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
     }
 #endif
   }
-  // Protocol health: a spin that timed out set the workgroup's abort word, and
-  // every logit of this launch is then suspect.  Each wave reports what it
-  // sees on exit to the handle's error word (host-visible; read by
-  // wk_check_device_errors / wk_stream_push): bit 0 = a spin timed out, bit 1 =
-  // the abort word holds a value no spin writes (LDS corruption).
-  if (lane == 0 && err) {
-    const unsigned ab = lds_load(reinterpret_cast<unsigned*>(smem + kCtrlOff) + kCtrlAbort);
-    if (ab) __hip_atomic_store(err, ab == 1u ? 1u : 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  report_abort(reinterpret_cast<unsigned*>(smem + kCtrlOff), err, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -867,7 +878,7 @@ template <int CM>
 __global__ __launch_bounds__(kFusedBlock, 4) void wk_cnn_fused_kernel(const float* __restrict__ feats, int64_t batch,
                                                                      const float* __restrict__ wts,
                                                                      const uint16_t* __restrict__ wbf,
-                                                                     float* __restrict__ logits) {
+                                                                     float* __restrict__ logits, unsigned* err) {
   __shared__ __attribute__((aligned(16))) float smem[kCnnLds];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -879,6 +890,7 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_cnn_fused_kernel(const floa
   const int64_t n_mine = batch > cb ? (batch - 1 - cb) / cs + 1 : 0;
   FeatSrc<CM> src = {feats, base, cb, cs, 0};
   cnn_role<CM>(base, wts, wbf, n_mine, cb, cs, logits, wave & 7, lane, src);
+  report_abort(reinterpret_cast<const unsigned*>(base + kCtrlOff), err, lane);   // this wave's role
 }
 
 }  // namespace
@@ -887,6 +899,17 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_cnn_fused_kernel(const floa
 extern "C" int wk_debug_logmel_set(float* fe, float* cnn) {
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_fe), &fe, sizeof(fe)) != hipSuccess) return 1;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_cnn), &cnn, sizeof(cnn)) != hipSuccess) return 1;
+  return 0;
+}
+#endif
+
+#ifdef WK_EPI_CHECK
+extern "C" int wk_debug_epi_get(unsigned* out8, int reset) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_epi_bad), 8 * sizeof(unsigned)) != hipSuccess) return 1;
+  if (reset) {
+    static unsigned zero[8];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_epi_bad), zero, sizeof(zero)) != hipSuccess) return 1;
+  }
   return 0;
 }
 #endif
@@ -934,20 +957,20 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
 }
 
 hipError_t launch_cnn_fused(const float* feats, int64_t batch, const float* w, const uint16_t* wbf, int conv_mode,
-                            float* logits, int grid_cap, hipStream_t stream) {
+                            float* logits, int grid_cap, hipStream_t stream, unsigned* err) {
   if (batch == 0) return hipSuccess;
   if (conv_mode != kConvF32 && !wbf) return hipErrorInvalidValue;
   const int64_t roles = (batch + NBF - 1) / NBF;   // at least one batch of clips per CNN role
   const int grid = (int)((roles + 1) / 2 < grid_cap ? (roles + 1) / 2 : grid_cap);
   if (conv_mode == kConvBf16)
     hipLaunchKernelGGL(wk_cnn_fused_kernel<kConvBf16>, dim3(grid), dim3(kFusedBlock), 0, stream, feats, batch, w, wbf,
-                       logits);
+                       logits, err);
   else if (conv_mode == kConvBf16x3)
     hipLaunchKernelGGL(wk_cnn_fused_kernel<kConvBf16x3>, dim3(grid), dim3(kFusedBlock), 0, stream, feats, batch, w,
-                       wbf, logits);
+                       wbf, logits, err);
   else
     hipLaunchKernelGGL(wk_cnn_fused_kernel<kConvF32>, dim3(grid), dim3(kFusedBlock), 0, stream, feats, batch, w, wbf,
-                       logits);
+                       logits, err);
   return hipGetLastError();
 }
 

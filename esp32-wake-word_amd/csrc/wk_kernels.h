@@ -48,7 +48,7 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
 // CNN on caller features (wk_fused.hip, the fused kernel's CNN role fed from
 // HBM): feats [B][13][63] -> logits [B]; conv_mode as launch_fused.
 hipError_t launch_cnn_fused(const float* feats, int64_t batch, const float* w, const uint16_t* wbf, int conv_mode,
-                            float* logits, int grid_cap, hipStream_t stream);
+                            float* logits, int grid_cap, hipStream_t stream, unsigned* err);
 
 // int8 CNN in the device's esp-dl arithmetic (wk_int8.hip); feats [B][13][63] fp32.
 constexpr int kNumInt8Weights = 3 * 13 * 32 + 3 * 32 * 64 + 3 * 64 * 128 + 128 * 64 + 64;

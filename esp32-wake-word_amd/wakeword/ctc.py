@@ -154,6 +154,15 @@ class CTCModel:
                                    C.c_void_p(ln.data_ptr()), self._stream(torch)), "wk_ctc_forward")
         return tok, ln, lp
 
+    def frame_argmax(self, batch: int, T: int):
+        """decode_predictions' per-frame `predictions` (ctc.py:454) of the last
+        decode/forward on this model: (batch, T) int32 on device."""
+        import torch
+        out = torch.empty((batch, T), dtype=torch.int32, device=f"cuda:{self.device}")
+        check(lib().wk_ctc_frame_argmax(self._h, batch, T, C.c_void_p(out.data_ptr()), self._stream(torch)),
+              "wk_ctc_frame_argmax")
+        return out
+
     def forward(self, feats, return_log_probs: bool = False):
         """(B, T, 80) -> token id lists (greedy CTC, decode_predictions'
         output form), and (B, T, V) log-probs if asked."""

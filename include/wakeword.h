@@ -86,9 +86,10 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
 wk_status wk_destroy(wk_handle* h);
 
 /* The fused kernel's two roles (front-end waves, CNN waves) hand clips over
- * through bounded spins; a spin that times out (a protocol failure -- never
- * expected) ends the launch with invalid logits instead of a hung GPU, and
- * raises a flag in a host-visible word of the handle.  This call synchronises
+ * through bounded spins, and the CNN role's waves (also behind wk_cnn)
+ * synchronise through bounded spins; a spin that times out (a protocol
+ * failure -- never expected) ends the launch with invalid logits instead of a
+ * hung GPU, and raises a flag in a host-visible word of the handle.  This call synchronises
  * the handle's device, returns WK_ERR_DEVICE if any launch on the handle since
  * the last check raised it (flags in *flags_out, may be NULL; 0 = clean), and
  * clears it.  wk_stream_push checks the word itself on every push. */
@@ -206,6 +207,12 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
  * handle's workspace grows on the first call with a larger batch*T. */
 wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T, float* d_log_probs_or_null,
                          int32_t* d_tokens, int32_t* d_lengths, void* stream);
+
+/* X3's per-frame argmax -- decode_predictions' `predictions` (ctc.py:454,
+ * first maximum per frame), the frame tokens the greedy decode collapsed --
+ * of the handle's last wk_ctc_forward: d_pred [batch][T] int32.  batch and T
+ * must be that call's (else WK_ERR_INVALID_ARG); stream-ordered after it. */
+wk_status wk_ctc_frame_argmax(wk_ctc* c, int64_t batch, int32_t T, int32_t* d_pred, void* stream);
 
 /* ---- WAV ingest and waveform augmentation (host only) ---
  * No device work: these fill caller (e.g. pinned) host buffers for the H2D copy. */

@@ -1,0 +1,164 @@
+"""Every BASELINE.json config at its stated size, through the C ABI, against the
+oracle.
+
+  config 1  single WAV CLI               tests/test_gpu_parity.py::test_cli_config1_golden_wavs
+  config 2  B = 65,536 fused fp32        tests/test_gpu_parity.py::test_full_size_batch_sample_parity
+  config 3  30 s stream, hop 480          test_config3_stream_30s_hop480 (below)
+  config 4  131,072 clips per rank, bf16  test_config4_bf16_rank_shard (below)
+  config 5  CTC B = 4096, T = 301, V = 4000, fp16   test_config5_ctc_full_batch (below)
+
+Sampled oracle parity at full size (a spread of windows / utterances through
+the CPU oracle), plus size-independent properties over the whole batch
+(finite outputs, decision agreement with the fp32 path, streaming == batch bit
+for bit, argmax-only tokens == log-prob-path tokens).  Tolerances are the
+ones stated in the per-path tests: fp32 logits 1e-3, bf16 0.05, CTC fp16
+log-probs 0.05 with identical argmax on frames whose oracle top-2 margin
+exceeds 0.2.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import wk_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_ATOL = 1e-3
+BF16_LOGIT_ATOL = 0.05
+CTC16_LOGP_ATOL = 0.05
+CTC16_MARGIN = 0.2
+WIN = 16000
+
+
+# ---------------------------------------------------------------- config 3
+def test_config3_stream_30s_hop480(gpu, golden_dir, xiaoa_sd):
+    """A continuous 30 s stream pushed 30 ms at a time (the hop), as a
+    device feeding the ring: every window is scored exactly once, in order,
+    bit-identical to the batch path over the same samples, and a spread of
+    windows matches the oracle."""
+    import ctypes as C
+    import torch
+    import wakeword
+    from wakeword import _lib
+    hop, seconds = 480, 30
+    audio = O.synth_clips(2024, 0, seconds).reshape(-1)           # 480,000 samples
+    n_win = (audio.size - WIN) // hop + 1
+    assert n_win == 967
+    model = wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"))
+    d = torch.from_numpy(audio).cuda()
+    ref = torch.empty(n_win, dtype=torch.float32, device="cuda")
+    _lib.check(_lib.lib().wk_forward(model._h.h, C.c_void_p(d.data_ptr()), _lib.WK_DTYPE_F32, n_win, WIN, hop,
+                                     C.c_void_p(ref.data_ptr()), None,
+                                     C.c_void_p(torch.cuda.current_stream().cuda_stream)), "wk_forward")
+    ref = ref.cpu().numpy()
+    det = wakeword.StreamingDetector(model, hop=hop, capacity=1 << 15)
+    ends, logits = [], []
+    for p in range(0, audio.size, hop):
+        for w in det.push(audio[p:p + hop]):
+            ends.append(w.end)
+            logits.append(w.logit)
+    det.close()
+    assert ends == [WIN + k * hop for k in range(n_win)]
+    np.testing.assert_array_equal(np.asarray(logits, np.float32), ref)
+    idx = np.linspace(0, n_win - 1, 8).astype(int)
+    clips = np.stack([audio[k * hop:k * hop + WIN] for k in idx]).astype(np.float64)
+    want = O.detect_mode_b(clips, xiaoa_sd)
+    assert np.abs(ref[idx] - want).max() < LOGIT_ATOL
+    model.check_device_errors()
+
+
+# ---------------------------------------------------------------- config 4
+def test_config4_bf16_rank_shard(gpu, golden_dir, xiaoa_sd):
+    """Config 4 at its per-rank size: 131,072 clips of rank 3's shard of the
+    1,048,576-clip job (global clip indices from weak_shard, so the device
+    generator gives the clips an 8-rank run scores there), bf16
+    convolutions.  All logits finite; a spread sample within 0.05 of the
+    oracle; every clip within 0.05 of the fp32 path with the same decision
+    wherever the fp32 logit is not within 0.05 of the threshold."""
+    import torch
+    import wakeword
+    from wakeword.shard import weak_shard
+    per_rank, rank = 131072, 3
+    first, count = weak_shard(per_rank, rank)
+    assert (first, count) == (rank * per_rank, per_rank)
+    x = wakeword.synth_clips(1234, first, count, device=0)
+    m16 = wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"), precision="bf16")
+    m32 = wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"))
+    a = m16.detect(x).reshape(-1)
+    b = m32.detect(x).reshape(-1)
+    m16.check_device_errors()
+    m32.check_device_errors()
+    assert bool(torch.isfinite(a).all()) and bool(torch.isfinite(b).all())
+    d = (a - b).abs()
+    assert d.max().item() <= BF16_LOGIT_ATOL, d.max().item()
+    confident = b.abs() > BF16_LOGIT_ATOL
+    assert bool(((a > 0) == (b > 0))[confident].all())
+    idx = np.linspace(0, count - 1, 16).astype(int)
+    xs = O.synth_clips(1234, first, 1, 16000)
+    assert np.abs(x[0].cpu().numpy() - xs[0]).max() < 1e-5   # device generator keyed on the global index
+    clips = x[torch.from_numpy(idx).cuda()].cpu().numpy().astype(np.float64)
+    ref = O.detect_mode_b(clips, xiaoa_sd)
+    a_np = a.cpu().numpy()
+    assert np.abs(a_np[idx] - ref).max() <= BF16_LOGIT_ATOL
+    assert np.abs(b.cpu().numpy()[idx] - ref).max() <= LOGIT_ATOL
+
+
+# ---------------------------------------------------------------- config 5
+def test_config5_ctc_full_batch():
+    """Config 5 at its bench size: B = 4096 utterances of 3 s (T = 301),
+    V = 4000, fp16.  The timed path (features -> decode, argmax-only output
+    kernel) and the log-prob path give identical tokens and lengths for all
+    4096 utterances; all lengths are in range and all log-probs finite; 16
+    utterances spread over the batch match the torch-CPU oracle (log-probs
+    within 0.05, argmax identical on frames whose oracle top-2 margin exceeds
+    0.2, and the greedy tokens equal to decode_predictions of the oracle for
+    every utterance whose frames are all that confident)."""
+    import torch
+    import wakeword
+    from oracle import wk_ctc_oracle as CO
+    B, V, n = 4096, 4000, 48000
+    T = 1 + n // 160
+    m = CO.make_model(V, seed=0)
+    g = wakeword.CTCModel(m.state_dict(), V, precision="fp16")
+    audio = wakeword.synth_clips(1234, 0, B, n)
+    feats = g.features(audio, n_samples=n)
+    assert feats.shape == (B, T, 80)
+    tok, ln, _ = g.decode(feats)
+    tok, ln = tok.clone(), ln.clone()
+    tok2, ln2, lp = g.decode(feats, return_log_probs=True)
+    assert torch.equal(ln, ln2) and torch.equal(tok, tok2)
+    assert int(ln.min()) >= 0 and int(ln.max()) <= T
+    assert bool(torch.isfinite(lp).all())
+    idx = torch.linspace(0, B - 1, 16).long()
+    x_s = torch.from_numpy(audio[idx.cuda()].cpu().numpy())
+    f_ref = CO.features(x_s)
+    np.testing.assert_allclose(feats[idx.cuda()].cpu().numpy(), f_ref.numpy(), atol=2e-3)
+    with torch.no_grad():
+        ref_lp = m(f_ref)
+    lp_s = lp[idx.cuda()].cpu()
+    del lp
+    assert np.abs((lp_s - ref_lp).numpy()).max() <= CTC16_LOGP_ATOL
+    top2 = torch.topk(ref_lp, 2, dim=-1).values
+    ok = (top2[..., 0] - top2[..., 1]) > CTC16_MARGIN
+    assert (lp_s.argmax(-1) == ref_lp.argmax(-1))[ok].all()
+    # per-frame argmax of the timed path (decode_predictions' `predictions`):
+    # the oracle's argmax on every confident frame, and the device tokens are
+    # exactly its blank-drop / repeat-collapse for all 4096 utterances
+    tok, ln, _ = g.decode(feats)
+    pred = g.frame_argmax(B, T)
+    pred_s = pred[idx.cuda()].cpu()
+    assert (pred_s == ref_lp.argmax(-1))[ok].all()
+    assert float(ok.float().mean()) > 0.1      # the sample has confident frames to check
+    p = pred.cpu().numpy()
+    keep = (p != 0) & (p != np.concatenate([np.zeros((B, 1), p.dtype), p[:, :-1]], axis=1))
+    tok_np, ln_np = tok.cpu().numpy(), ln.cpu().numpy()
+    np.testing.assert_array_equal(ln_np, keep.sum(1))
+    assert np.array_equal(tok_np[np.arange(T)[None, :] < ln_np[:, None]], p[keep])
+    assert (tok_np[np.arange(T)[None, :] >= ln_np[:, None]] == -1).all()
+    # and where the oracle's whole utterance is confident, the tokens are its greedy decode
+    ref_seqs = CO.greedy_decode(ref_lp)
+    for j in range(len(idx)):
+        if bool(ok[j].all()):
+            b = int(idx[j])
+            assert tok_np[b, :ln_np[b]].tolist() == ref_seqs[j]

@@ -23,6 +23,9 @@ def test_error_word_clean_at_scale(gpu, golden_dir, precision):
     x = wakeword.synth_clips(99, 0, 65536, device=0)
     for _ in range(3):
         m.detect(x)
+    feats = wakeword.mfcc(x[:8192])
+    for _ in range(3):
+        m(feats)                # wk_cnn: the same CNN role, two per workgroup, reports to the same word
     flags = C.c_uint32(123)
     assert _lib.lib().wk_check_device_errors(m._h.h, C.byref(flags)) == 0
     assert flags.value == 0
