@@ -239,8 +239,11 @@ wk_status wk_cnn(wk_handle* h, const float* d_feats, int64_t batch, float* d_log
   });
 }
 
-wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len,
-                     int64_t clip_stride, float* d_logits, float* d_feats_or_null, void* stream) {
+// wk_forward with the error word the launches report to: the handle's
+// (wk_forward) or a stream object's own (wk_stream_push).
+static wk_status forward_impl(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len,
+                              int64_t clip_stride, float* d_logits, float* d_feats_or_null, void* stream,
+                              unsigned* d_err) {
   if (!h) return invalid("wk_forward: null handle");
   if (h->cfg.mode != WK_MODE_TORCHAUDIO_CMVN) {
     g_last_error = "wk_forward: the xiaoa CNN consumes mode-B (torchaudio+CMVN) features";
@@ -254,7 +257,7 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
   return on_device(h->cfg.device, [&]() -> wk_status {
     if (!h->unfused && !int8) {
       hipError_t e = wk::launch_fused(dtype == WK_DTYPE_I16, d_audio, batch, clip_stride, h->d_packed, h->d_bf16,
-                                      conv_mode_of(h), d_logits, d_feats_or_null, h->n_cu, (hipStream_t)stream, h->d_err,
+                                      conv_mode_of(h), d_logits, d_feats_or_null, h->n_cu, (hipStream_t)stream, d_err,
                                       h->fused_exp);
       return e == hipSuccess ? WK_OK : hip_fail(e, "fused launch");
     }
@@ -267,25 +270,40 @@ wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t b
       hipError_t e = h->ws_used ? hipStreamWaitEvent((hipStream_t)stream, h->ws_free, 0) : hipSuccess;
       if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent(workspace)");
     }
+    // Every exit after the first launch (a failed later launch included) marks
+    // the workspace busy until this stream's queued chunks are done, so the next
+    // call on another stream still waits for them.
+    bool launched = false;
+    struct WsRelease {
+      wk_handle* h;
+      std::unique_lock<std::mutex>& lk;
+      bool& launched;
+      hipStream_t st;
+      ~WsRelease() {
+        if (lk.owns_lock() && launched && hipEventRecord(h->ws_free, st) == hipSuccess) h->ws_used = true;
+      }
+    } ws_release{h, ws_lock, launched, (hipStream_t)stream};
     for (int64_t c0 = 0; c0 < batch; c0 += h->ws_clips) {
       const int64_t n = batch - c0 < h->ws_clips ? batch - c0 : h->ws_clips;
       float* feats = d_feats_or_null ? d_feats_or_null + c0 * 13 * 63 : h->d_feats_ws;
       const void* a = (const char*)d_audio + (size_t)(c0 * clip_stride) * esz;
+      launched = true;   // (a failed launch may still have queued work)
       hipError_t e = wk::launch_frontend(true, dtype == WK_DTYPE_I16, a, n, win_len, clip_stride, feats, 0, 1,
                                          2 * h->n_cu, 0.97f, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(e, "frontend launch");
       e = int8 ? wk::launch_int8_cnn(feats, n, h->d_int8, d_logits + c0, 4 * h->n_cu, (hipStream_t)stream)
                : wk::launch_cnn_fused(feats, n, h->d_packed, h->d_bf16, conv_mode_of(h), d_logits + c0, h->n_cu,
-                                      (hipStream_t)stream, h->d_err);
+                                      (hipStream_t)stream, d_err);
       if (e != hipSuccess) return hip_fail(e, "cnn launch");
-    }
-    if (ws_lock.owns_lock()) {
-      hipError_t e = hipEventRecord(h->ws_free, (hipStream_t)stream);
-      if (e != hipSuccess) return hip_fail(e, "hipEventRecord(workspace)");
-      h->ws_used = true;
     }
     return WK_OK;
   });
+}
+
+wk_status wk_forward(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batch, int32_t win_len,
+                     int64_t clip_stride, float* d_logits, float* d_feats_or_null, void* stream) {
+  return forward_impl(h, d_audio, dtype, batch, win_len, clip_stride, d_logits, d_feats_or_null, stream,
+                      h ? h->d_err : nullptr);
 }
 
 wk_status wk_synth_clips(uint32_t seed, int64_t first, int64_t count, int32_t n, float* d_out, void* stream) {
@@ -300,6 +318,22 @@ wk_status wk_normalize(const float* d_in, float* d_out, int64_t batch, int32_t n
   if (batch > 0 && (!d_in || !d_out)) return invalid("wk_normalize: null pointer");
   hipError_t e = wk::launch_normalize(d_in, d_out, batch, n_coef, n_time, method, (hipStream_t)stream);
   return e == hipSuccess ? WK_OK : hip_fail(e, "normalize launch");
+}
+
+wk_status wk_record_front(const int16_t* d_tdm, int64_t n_out, int16_t* d_out16, float* d_out_f32_or_null,
+                          void* stream) {
+  if (n_out < 0 || (n_out > 0 && (!d_tdm || !d_out16))) return invalid("wk_record_front: bad arguments");
+  if (n_out > 1 && ((uintptr_t)d_tdm & 15)) return invalid("wk_record_front: d_tdm must be 16-byte aligned");
+  if (((uintptr_t)d_out16 & 3) || ((uintptr_t)d_out_f32_or_null & 7))
+    return invalid("wk_record_front: d_out16 must be 4-byte and d_out_f32 8-byte aligned");
+  hipError_t e = wk::launch_record_front(d_tdm, n_out, d_out16, d_out_f32_or_null, (hipStream_t)stream);
+  return e == hipSuccess ? WK_OK : hip_fail(e, "record_front launch");
+}
+
+wk_status wk_quantize_frames(const float* d_mfcc, int64_t n_values, int8_t* d_out_i8, void* stream) {
+  if (n_values < 0 || (n_values > 0 && (!d_mfcc || !d_out_i8))) return invalid("wk_quantize_frames: bad arguments");
+  hipError_t e = wk::launch_quantize_frames(d_mfcc, n_values, d_out_i8, (hipStream_t)stream);
+  return e == hipSuccess ? WK_OK : hip_fail(e, "quantize_frames launch");
 }
 
 wk_status wk_device_cmvn(const void* d_frames, int32_t dtype, int64_t n_frames, int8_t* d_out_i8,
@@ -478,6 +512,8 @@ struct wk_stream {
   float* d_stage;       // device [2*cap]: backlog runs are copied here first
   float* h_logits;      // pinned, mapped [max_win] (written by the kernel)
   float* a_logits;      // device alias of h_logits
+  unsigned* h_err;      // pinned, mapped: this stream object's own error word (its pushes' launches only)
+  unsigned* d_err;      // device alias of h_err
   int32_t max_win;
 };
 
@@ -485,6 +521,7 @@ static void stream_free(wk_stream* s) {
   (void)hipHostFree(s->h_ring);
   (void)hipFree(s->d_stage);
   (void)hipHostFree(s->h_logits);
+  (void)hipHostFree(s->h_err);
   free(s);
 }
 
@@ -508,11 +545,14 @@ wk_status wk_stream_create(wk_handle* h, int32_t hop, int32_t capacity, void* st
         (e = hipHostGetDevicePointer((void**)&s->a_ring, s->h_ring, 0)) != hipSuccess ||
         (e = hipMalloc(&s->d_stage, sizeof(float) * 2 * (size_t)capacity)) != hipSuccess ||
         (e = hipHostMalloc(&s->h_logits, sizeof(float) * (size_t)s->max_win, mapped)) != hipSuccess ||
-        (e = hipHostGetDevicePointer((void**)&s->a_logits, s->h_logits, 0)) != hipSuccess) {
+        (e = hipHostGetDevicePointer((void**)&s->a_logits, s->h_logits, 0)) != hipSuccess ||
+        (e = hipHostMalloc(&s->h_err, sizeof(unsigned), mapped)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&s->d_err, s->h_err, 0)) != hipSuccess) {
       stream_free(s);
       return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_stream_create");
     }
     memset(s->h_ring, 0, sizeof(float) * 2 * (size_t)capacity);
+    *s->h_err = 0;
     *out = s;
     return WK_OK;
   });
@@ -564,10 +604,20 @@ wk_status wk_stream_push(wk_stream* s, const float* samples, int64_t n, float* o
   const int64_t k = last - first + 1;
   if (k <= 0) return WK_OK;
   return on_device(s->h->cfg.device, [&]() -> wk_status {
-    // 3. score them: contiguous strided runs in the mirrored ring.
+    // 3. score them: contiguous strided runs in the mirrored ring.  On any
+    // failure after the first launch the stream is drained before returning,
+    // so no kernel is still reading the host ring when the next push rewrites it.
+    struct Drain {
+      hipStream_t st;
+      bool armed = false;
+      ~Drain() {
+        if (armed) (void)hipStreamSynchronize(st);
+      }
+    } drain{s->st};
     hipError_t e;
     int64_t w = first;
     while (w <= last) {
+      drain.armed = true;
       const int64_t off = (w * s->hop) % cap;
       int64_t run = (2 * cap - WK_WIN_SAMPLES - off) / s->hop + 1;   // windows that fit before the mirror end
       if (run > last - w + 1) run = last - w + 1;
@@ -579,15 +629,17 @@ wk_status wk_stream_push(wk_stream* s, const float* samples, int64_t n, float* o
           return hip_fail(e, "wk_stream_push: H2D");
         src = s->d_stage;
       }
-      wk_status st = wk_forward(s->h, src, WK_DTYPE_F32, run, WK_WIN_SAMPLES, s->hop, s->a_logits + (w - first),
-                                nullptr, s->st);
+      wk_status st = forward_impl(s->h, src, WK_DTYPE_F32, run, WK_WIN_SAMPLES, s->hop, s->a_logits + (w - first),
+                                  nullptr, s->st, s->d_err);
       if (st != WK_OK) return st;
       if (run > kZeroCopyMax && (e = hipStreamSynchronize(s->st)) != hipSuccess)   // d_stage is reused
         return hip_fail(e, "wk_stream_push: sync");
       w += run;
     }
     if ((e = hipStreamSynchronize(s->st)) != hipSuccess) return hip_fail(e, "wk_stream_push: sync");
-    if (const uint32_t f = __atomic_exchange_n(s->h->h_err, 0u, __ATOMIC_SEQ_CST)) {   // synced: the word is final
+    drain.armed = false;
+    // synced, and only this stream object's launches report to its word: final
+    if (const uint32_t f = __atomic_exchange_n(s->h_err, 0u, __ATOMIC_SEQ_CST)) {
       g_last_error = "fused kernel protocol error (flags " + std::to_string(f) + "): these logits are invalid";
       return WK_ERR_DEVICE;
     }

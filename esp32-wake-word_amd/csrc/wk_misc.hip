@@ -1,4 +1,5 @@
-// wk_misc.hip -- device-side synthetic clip generator and normalize_mfcc.
+// wk_misc.hip -- device-side synthetic clip generator, normalize_mfcc, and the
+// firmware's sample / frame front (record_task) and per-window CMVN (detect_task).
 #include "wk_common.h"
 #include "wk_kernels.h"
 
@@ -119,9 +120,76 @@ __global__ void wk_device_cmvn_kernel(const T* __restrict__ frames, int64_t n_wi
   }
 }
 
+// The firmware record task's sample path (esp_wake_word_detector.cpp:102-121),
+// integer-exact: 48 kHz TDM frames of 4 int16 channels (CH0 MIC-L, CH1 AEC
+// reference, CH2 MIC-R, CH3 unused) -> mono
+//   m = (int16_t)(((L << 6) + (AEC << 5) + (R << 6)) >> 7)   (:106-111)
+// -- the int32 sum can exceed int16 (|L| = |R| = 32767 gives 40958) and the
+// firmware's cast keeps the low 16 bits, so does this -- then the [1, 2, 1] / 4
+// decimation to 16 kHz: out[j] = (int16_t)((m[3j] + 2 m[3j+1] + m[3j+2]) >> 2)
+// (:114-121; >> on int32 is arithmetic, as on the ESP32).  Each thread makes
+// two output samples from six TDM samples = 48 contiguous bytes, three 16-byte
+// loads (HBM-bound byte work: 24 B in, 2 B out (+4 with the float copy) per
+// output sample).  The float copy is x / 32768 (torchaudio.load's scale, what
+// wk_forward applies to WK_DTYPE_I16).
+__device__ __forceinline__ int32_t tdm_mono(uint2 q) {   // one TDM sample: 4 int16 channels in 8 bytes
+  const int32_t l = (int16_t)(q.x & 0xFFFFu), aec = (int16_t)(q.x >> 16), r = (int16_t)(q.y & 0xFFFFu);
+  return (int16_t)((l * 64 + aec * 32 + r * 64) >> 7);
+}
+__device__ __forceinline__ int16_t tdm_out(int32_t m0, int32_t m1, int32_t m2) {
+  return (int16_t)((m0 + 2 * m1 + m2) >> 2);
+}
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void wk_record_front_kernel(const u32x4* __restrict__ tdm, int64_t n_out,
+                                                              int16_t* __restrict__ out16, float* __restrict__ outf) {
+  const int64_t pair = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t j = 2 * pair;
+  if (j >= n_out) return;
+  int16_t o[2];
+  if (j + 1 < n_out) {
+    const u32x4 a = __builtin_nontemporal_load(tdm + 3 * pair);
+    const u32x4 b = __builtin_nontemporal_load(tdm + 3 * pair + 1);
+    const u32x4 c = __builtin_nontemporal_load(tdm + 3 * pair + 2);
+    o[0] = tdm_out(tdm_mono(make_uint2(a.x, a.y)), tdm_mono(make_uint2(a.z, a.w)), tdm_mono(make_uint2(b.x, b.y)));
+    o[1] = tdm_out(tdm_mono(make_uint2(b.z, b.w)), tdm_mono(make_uint2(c.x, c.y)), tdm_mono(make_uint2(c.z, c.w)));
+    *reinterpret_cast<uint32_t*>(out16 + j) = (uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16);
+    if (outf) *reinterpret_cast<float2*>(outf + j) = make_float2(o[0] * (1.0f / 32768.0f), o[1] * (1.0f / 32768.0f));
+  } else {   // odd tail: the last output sample alone (three 8-byte TDM samples)
+    const uint2* q = reinterpret_cast<const uint2*>(tdm) + 3 * j;
+    o[0] = tdm_out(tdm_mono(q[0]), tdm_mono(q[1]), tdm_mono(q[2]));
+    out16[j] = o[0];
+    if (outf) outf[j] = o[0] * (1.0f / 32768.0f);
+  }
+}
+
+// record_task's int8 frame quantisation (:128-131): lroundf (half away from
+// zero), saturate to [-128, 127].
+__global__ __launch_bounds__(256) void wk_quantize_frames_kernel(const float* __restrict__ x, int64_t n,
+                                                                 int8_t* __restrict__ q) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    q[i] = (int8_t)device_q(x[i]);
+}
+
 }  // namespace
 
 namespace wk {
+
+hipError_t launch_record_front(const int16_t* tdm, int64_t n_out, int16_t* out16, float* outf, hipStream_t stream) {
+  if (n_out <= 0) return hipSuccess;
+  const int64_t pairs = (n_out + 1) / 2;
+  hipLaunchKernelGGL(wk_record_front_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const u32x4*>(tdm), n_out, out16, outf);
+  return hipGetLastError();
+}
+
+hipError_t launch_quantize_frames(const float* x, int64_t n, int8_t* q, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(wk_quantize_frames_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, n, q);
+  return hipGetLastError();
+}
 
 hipError_t launch_device_cmvn(const void* frames, bool int8_in, int64_t n_windows, int8_t* out_i8, float* out_f,
                               hipStream_t stream) {

@@ -9,7 +9,7 @@ from .api import (KWSModel, detect, extract_mfcc, load_onnx, load_wav, mfcc, nor
                   pad_audio, synth_clips)
 from .onnx_reader import read_onnx, xiaoa_state_dict  # noqa: F401
 from .stream import (DecisionRule, DeviceDetector, FrameDecisionLoop, FrameWindow, StreamingDetector,  # noqa: F401
-                     Window, device_cmvn)
+                     Window, device_cmvn, quantize_frames, record_front)
 from .ctc import CTCModel, ctc_state_dict_spec, decode_predictions, pack_state_dict, tokens_to_text  # noqa: F401
 from . import wav  # noqa: F401
 

@@ -101,6 +101,43 @@ FRAME_WIN = 63           # frames per window (MFCC_LEN = 13*63, :3)
 N_COEF = 13
 
 
+def record_front(tdm, device: int = 0, float_out: bool = False):
+    """wk_record_front: the firmware record task's sample path
+    (esp_wake_word_detector.cpp:102-121) on device.  tdm: int16 48 kHz TDM
+    samples of 4 channels, shape (n, 4), (frames, 960, 4) or flat (4n,), n a
+    multiple of 3 -> int16 16 kHz samples (n // 3,) on device (and the same
+    / 32768 as float32 when float_out)."""
+    import torch
+    x = tdm
+    if isinstance(x, np.ndarray):
+        x = torch.from_numpy(np.ascontiguousarray(x))
+    if x.dtype != torch.int16:
+        raise ValueError(f"TDM samples must be int16, got {x.dtype}")
+    x = x.to(f"cuda:{device}").contiguous().reshape(-1)
+    if x.numel() % 12:
+        raise ValueError("TDM input must hold whole groups of 3 samples x 4 channels")
+    n_out = x.numel() // 12
+    out = torch.empty((n_out,), dtype=torch.int16, device=x.device)
+    f = torch.empty((n_out,), dtype=torch.float32, device=x.device) if float_out else None
+    st = torch.cuda.current_stream(x.device)
+    check(lib().wk_record_front(C.c_void_p(x.data_ptr()), n_out, C.c_void_p(out.data_ptr()),
+                                C.c_void_p(f.data_ptr()) if f is not None else None, C.c_void_p(st.cuda_stream)),
+          "wk_record_front")
+    return (out, f) if float_out else out
+
+
+def quantize_frames(mfcc, device: int = 0):
+    """wk_quantize_frames: record_task's int8 frame quantisation (:128-131),
+    lroundf then saturate -> int8 tensor of mfcc's shape, on device."""
+    import torch
+    x = torch.as_tensor(mfcc, dtype=torch.float32).to(f"cuda:{device}").contiguous()
+    q = torch.empty(x.shape, dtype=torch.int8, device=x.device)
+    st = torch.cuda.current_stream(x.device)
+    check(lib().wk_quantize_frames(C.c_void_p(x.data_ptr()), x.numel(), C.c_void_p(q.data_ptr()),
+                                   C.c_void_p(st.cuda_stream)), "wk_quantize_frames")
+    return q
+
+
 def device_cmvn(frames, device: int = 0):
     """wk_device_cmvn on an MFCC frame stream [n][13] (int8 as the firmware
     stores it, or float MFCC quantised first as record_task :128-131 does):

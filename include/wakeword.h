@@ -92,7 +92,8 @@ wk_status wk_destroy(wk_handle* h);
  * hung GPU, and raises a flag in a host-visible word of the handle.  This call synchronises
  * the handle's device, returns WK_ERR_DEVICE if any launch on the handle since
  * the last check raised it (flags in *flags_out, may be NULL; 0 = clean), and
- * clears it.  wk_stream_push checks the word itself on every push. */
+ * clears it.  A wk_stream has its own word (its pushes' launches report there,
+ * not to the handle's): wk_stream_push checks and clears it on every push. */
 wk_status wk_check_device_errors(wk_handle* h, uint32_t* flags_out);
 
 /* Front-end only.  d_audio: `batch` clips of `win_len` samples, clip i at
@@ -169,6 +170,25 @@ wk_status wk_stream_push(wk_stream* s, const float* host_samples, int64_t n, flo
  * Bit-identical to the firmware's C loops (same fp32 summation order). */
 wk_status wk_device_cmvn(const void* d_frames, int32_t dtype, int64_t n_frames, int8_t* d_out_i8,
                          float* d_feats_or_null, void* stream);
+
+/* ---- The firmware record task's front (esp_wake_word_detector.cpp:52-150) ---
+ * wk_record_front: the sample path of record_task (:102-121), integer-exact.
+ * d_tdm holds 3*n_out 48 kHz TDM samples of 4 int16 channels (interleaved
+ * CH0 MIC-L, CH1 AEC reference, CH2 MIC-R, CH3 unused; the firmware reads 960
+ * of them = 3840 int16 per 20 ms frame); per TDM sample the mono mix
+ * m = (int16_t)(((L<<6) + (AEC<<5) + (R<<6)) >> 7) keeps the low 16 bits of the
+ * int32 sum as the firmware's cast does; then d_out16[j] =
+ * (int16_t)((m[3j] + 2 m[3j+1] + m[3j+2]) >> 2) at 16 kHz (320 per frame).
+ * Frames are independent of each other (960 = 3 x 320), so any run of frames
+ * is one call.  d_out_f32_or_null receives d_out16 / 32768.  d_out16 can feed
+ * wk_forward directly as WK_DTYPE_I16 (clip_stride = hop: sliding windows);
+ * the esp-dl MFCC the firmware runs on it (:124-125) is third-party and absent.
+ * Alignment: d_tdm 16 bytes, d_out16 4, d_out_f32 8. */
+wk_status wk_record_front(const int16_t* d_tdm, int64_t n_out, int16_t* d_out16, float* d_out_f32_or_null,
+                          void* stream);
+/* record_task's frame quantisation (:128-131): d_out_i8[i] = saturate_int8(lroundf(d_mfcc[i])),
+ * n_values = 13 x frames; the result feeds wk_device_cmvn as WK_DTYPE_I8. */
+wk_status wk_quantize_frames(const float* d_mfcc, int64_t n_values, int8_t* d_out_i8, void* stream);
 
 /* ---- CTC head (ml_models/ctc.py) -------------------------
  * GRU_CTC_Model (ctc.py:119-152) + its log-mel front-end (ctc.py:82-107) +

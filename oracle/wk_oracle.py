@@ -348,6 +348,36 @@ def quantize_input(feats: np.ndarray) -> np.ndarray:
 # are each IEEE-rounded, in the firmware's loop order, so the int8 results are
 # the C loops' results bit for bit.
 # --------------------------------------------------------------------------
+def record_front(tdm: np.ndarray) -> np.ndarray:
+    """record_task's sample path, esp_wake_word_detector.cpp:102-121, in int32
+    like the C: tdm int16 [..., 4] 48 kHz TDM samples (CH0 MIC-L, CH1 AEC ref,
+    CH2 MIC-R, CH3 unused), a multiple of 3 of them -> int16 16 kHz samples.
+      :106-111  weighted = (L<<6) + (AEC<<5) + (R<<6);  mono = (int16_t)(weighted >> 7)
+      :114-121  out = (int16_t)((mono[3i] + 2 mono[3i+1] + mono[3i+2]) >> 2)
+    The int16 casts keep the low 16 bits (numpy's int32 -> int16 cast wraps the
+    same way); >> on int32 is arithmetic in both."""
+    q = np.asarray(tdm, np.int16).reshape(-1, 4).astype(np.int32)
+    assert q.shape[0] % 3 == 0, "whole groups of 3 TDM samples"
+    weighted = (q[:, 0] << 6) + (q[:, 1] << 5) + (q[:, 2] << 6)
+    mono = (weighted >> 7).astype(np.int16).astype(np.int32)
+    m = mono.reshape(-1, 3)
+    return ((m[:, 0] * 1 + m[:, 1] * 2 + m[:, 2] * 1) >> 2).astype(np.int16)
+
+
+def record_front_loop(tdm_frame: np.ndarray) -> np.ndarray:
+    """The same for one 20 ms frame (3840 int16), statement by statement as the
+    C loops run (small inputs only; pins record_front)."""
+    def i16(v):
+        return ((int(v) + 32768) % 65536) - 32768
+    x = [int(v) for v in np.asarray(tdm_frame, np.int16).reshape(-1)]
+    mono = []
+    for i in range(len(x) // 4):
+        weighted = x[i * 4] * 64 + x[i * 4 + 1] * 32 + x[i * 4 + 2] * 64    # (int32)v << k == v * 2^k
+        mono.append(i16(weighted >> 7))                                     # Python >> is arithmetic
+    return np.array([i16((mono[3 * i] + 2 * mono[3 * i + 1] + mono[3 * i + 2]) >> 2) for i in range(len(mono) // 3)],
+                    np.int16)
+
+
 def device_quantize_frames(mfcc: np.ndarray) -> np.ndarray:
     """record_task :128-131: (int32_t)lroundf(v), saturated to int8."""
     v = np.asarray(mfcc, np.float32).astype(np.float64)
