@@ -167,6 +167,7 @@ class FrameWindow:
     logit: float      # model output (int8 model: raw * 2^-3, as the firmware dequantises it, :226-227)
     pct: float        # sigmoid * 100 (:228)
     detected: bool
+    cleared: bool = False   # the post-sleep inference on the just-cleared (all-zero) ring
 
 
 class FrameDecisionLoop:
@@ -177,25 +178,35 @@ class FrameDecisionLoop:
     the window is the newest 63); sigmoid*100 >= threshold fires (:245); the
     task then sleeps 5 s = `deaf_frames` frames of 20 ms (:248) and clears the
     ring (:251-256), so the next window needs 64 frames written after that.
-    (The firmware also runs one extra inference on the just-cleared buffer
-    when it wakes, from the notification left pending during the sleep; it is
-    not modelled.)"""
 
-    def __init__(self, threshold_pct: float = 80.0, deaf_frames: int = 250):
+    The extra inference after each sleep (cleared_inference=True): record_task
+    keeps notifying while detect_task sleeps (:141-143), so right after the
+    reset ulTaskNotifyTake (:172) returns at once and the task scores the
+    cleared ring -- all zeros, since the reset and that read fall in one 20 ms
+    frame period -- as a window at the wake frame (fire frame + deaf_frames).
+    `pending` is that frame until it is scored; a firing extra inference sleeps
+    and clears again."""
+
+    def __init__(self, threshold_pct: float = 80.0, deaf_frames: int = 250, cleared_inference: bool = True):
         self.threshold = np.float32(threshold_pct)
         self.deaf = deaf_frames
+        self.cleared_inference = cleared_inference
         self.reset_at = 0          # first frame written after the last reset
+        self.pending: Optional[int] = None
 
     def scored(self, e: int) -> bool:
         return e - self.reset_at >= FRAME_WIN
 
-    def __call__(self, e: int, logit: float) -> FrameWindow:
+    def __call__(self, e: int, logit: float, cleared: bool = False) -> FrameWindow:
         x = np.float32(logit)
         pct = np.float32(1.0) / (np.float32(1.0) + np.exp(-x)) * np.float32(100.0)
         fire = bool(pct >= self.threshold)
+        if cleared:
+            self.pending = None
         if fire:
             self.reset_at = e + self.deaf + 1
-        return FrameWindow(e, float(x), float(pct), fire)
+            self.pending = e + self.deaf if self.cleared_inference else None
+        return FrameWindow(e, float(x), float(pct), fire, cleared)
 
 
 class DeviceDetector:
@@ -207,11 +218,25 @@ class DeviceDetector:
     from esp-dl's dl::audio::MFCC on the device (a third-party library absent
     here): the caller supplies them, int8 or float."""
 
-    def __init__(self, model, threshold_pct: float = 80.0, refractory_s: float = 5.0, frame_s: float = 0.02):
+    def __init__(self, model, threshold_pct: float = 80.0, refractory_s: float = 5.0, frame_s: float = 0.02,
+                 cleared_inference: bool = True):
         self._model = model
-        self.loop = FrameDecisionLoop(threshold_pct, int(round(refractory_s / frame_s)))
+        self.loop = FrameDecisionLoop(threshold_pct, int(round(refractory_s / frame_s)), cleared_inference)
         self._tail = None          # the last <= 62 frames of earlier pushes
         self._next = 0             # index of the next frame to arrive
+        self._zero_logit = None    # the model on the CMVN of an all-zero ring (computed once)
+
+    def cleared_logit(self) -> float:
+        """The model's output on the cleared ring (63 zero frames through the
+        device CMVN: all zeros), scored after every sleep."""
+        if self._zero_logit is None:
+            _, feats = device_cmvn(np.zeros((FRAME_WIN, N_COEF), np.int8), self._model.device)
+            self._zero_logit = float(self._model(feats).reshape(-1)[0])
+        return self._zero_logit
+
+    def _due(self, before: int, out: List[FrameWindow]) -> None:
+        while self.loop.pending is not None and self.loop.pending < before:
+            out.append(self.loop(self.loop.pending, self.cleared_logit(), cleared=True))
 
     def push(self, frames) -> List[FrameWindow]:
         f = np.asarray(frames)
@@ -226,14 +251,15 @@ class DeviceDetector:
         self._next += f.shape[0]
         self._tail = cat[-(FRAME_WIN - 1):].copy()
         out: List[FrameWindow] = []
-        if cat.shape[0] < FRAME_WIN:
-            return out
         ends = np.arange(first + FRAME_WIN - 1, first + cat.shape[0])
-        if not any(self.loop.scored(int(e)) for e in ends):   # (reset_at only grows during the walk)
+        if cat.shape[0] < FRAME_WIN or not any(self.loop.scored(int(e)) for e in ends):
+            self._due(self._next, out)   # (reset_at only grows during the walk)
             return out
         _, feats = device_cmvn(cat, self._model.device)
         logits = self._model(feats).reshape(-1).cpu().numpy()
         for e, lg in zip(ends, logits):
+            self._due(int(e), out)
             if self.loop.scored(int(e)):
                 out.append(self.loop(int(e), float(lg)))
+        self._due(self._next, out)
         return out

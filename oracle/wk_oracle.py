@@ -407,25 +407,47 @@ def device_cmvn(frames: np.ndarray) -> np.ndarray:
     return device_quantize_frames(nrm)
 
 
-def device_decisions(n_frames: int, logits: np.ndarray, threshold_pct: float = 80.0, deaf_frames: int = 250):
+def device_decisions(n_frames: int, logits: np.ndarray, threshold_pct: float = 80.0, deaf_frames: int = 250,
+                     cleared_logit: float | None = None):
     """detect_task's control flow (:171-258) in the frame domain, as a plain loop:
     the window ending at frame e (frames e-62..e) is scored once 64 frames were
     written since the last reset (shared_counter == 64, :38-44,141); a score
     sigmoid(x)*100 >= 80 (:228,245) fires, the task sleeps 5 s (250 frames of 20
     ms, :248) and then clears the buffer (:251-256).  logits[e - 62] is the
-    window ending at frame e.  Returns (end_frame, detected) of every scored window."""
+    window ending at frame e.  Returns (end_frame, detected) of every scored window.
+
+    cleared_logit (the model's output on the CMVN of an all-zero ring): the
+    firmware's extra inference after each sleep.  record_task keeps calling
+    xTaskNotifyGive (:141-143) while detect_task sleeps, so when it has cleared
+    the ring its ulTaskNotifyTake (:172) returns at once and it scores the
+    cleared buffer -- all zeros: the reset and that read happen within the same
+    20 ms frame period -- as the window "ending" at the wake frame x + 250.  If
+    that fires too, it sleeps and clears again."""
+    def fires(x):
+        x = np.float32(x)
+        pct = np.float32(1.0) / (np.float32(1.0) + np.exp(-x)) * np.float32(100.0)
+        return bool(pct >= np.float32(threshold_pct))
+
     out, reset = [], 0
     e = 62
     while e < n_frames:
         if e - reset < 63:
             e += 1
             continue
-        x = np.float32(logits[e - 62])
-        pct = np.float32(1.0) / (np.float32(1.0) + np.exp(-x)) * np.float32(100.0)
-        fire = bool(pct >= np.float32(threshold_pct))
+        fire = fires(logits[e - 62])
         out.append((e, fire))
         if fire:
-            reset = e + deaf_frames + 1
+            x = e
+            while True:
+                wake = x + deaf_frames
+                reset = wake + 1
+                if cleared_logit is None or wake >= n_frames:
+                    break
+                again = fires(cleared_logit)
+                out.append((wake, again))
+                if not again:
+                    break
+                x = wake
             e = reset
             continue
         e += 1

@@ -98,6 +98,42 @@ def test_decision_loop_matches_oracle():
     assert want[0][0] == 63                                      # the 64th frame completes the first window
 
 
+def _walk(loop, n, logits, zero_logit):
+    """DeviceDetector's order of events on precomputed window logits (host only)."""
+    got = []
+    for e in range(62, n):
+        while loop.pending is not None and loop.pending < e:
+            w = loop(loop.pending, zero_logit, cleared=True)
+            got.append((w.end, w.detected))
+        if loop.scored(e):
+            w = loop(e, float(logits[e - 62]))
+            got.append((w.end, w.detected))
+    while loop.pending is not None and loop.pending < n:
+        w = loop(loop.pending, zero_logit, cleared=True)
+        got.append((w.end, w.detected))
+    return got
+
+
+@pytest.mark.parametrize("zero_logit", [-4.0, 3.0])
+def test_post_sleep_inference_on_the_cleared_ring(zero_logit):
+    """After each 5 s sleep the firmware scores the just-cleared (all-zero)
+    ring once (pending notification, :141-143,172,248-257): one extra window
+    at the wake frame; if it fires, another sleep and another extra window."""
+    r = np.random.default_rng(4)
+    n = 3000
+    logits = r.normal(-4, 1, n - 62).astype(np.float32)
+    logits[[100, 101, 400, 700, 701, 2900]] = 3.0
+    want = O.device_decisions(n, logits, cleared_logit=zero_logit)
+    assert _walk(FrameDecisionLoop(), n, logits, zero_logit) == want
+    fired = [e for e, d in want if d]
+    assert (162 + 250, zero_logit > 0) in want                 # the wake frame's extra window
+    if zero_logit > 0:                                           # fires again every 250 frames to the end
+        assert fired == list(range(162, n, 250))
+    else:
+        assert fired[0] == 162 and (412, False) in want and fired[1] >= 412 + 1 + 63
+    assert _walk(FrameDecisionLoop(cleared_inference=False), n, logits, zero_logit) == O.device_decisions(n, logits)
+
+
 def test_decision_threshold_is_sigmoid_percent():
     loop = FrameDecisionLoop()
     w = loop(63, math.log(4.0) - 1e-4)       # sigmoid = 0.8 - eps
@@ -143,9 +179,12 @@ def test_gpu_device_pipeline_int8_logits(gpu, golden_dir, xiaoa_sd):
     c = O.device_cmvn(f)
     want = O.kws_forward_int8(O.quantize_input(c.transpose(0, 2, 1).astype(np.float64)), O.quantize_int8(xiaoa_sd))
     want = (want * 0.125).astype(np.float32)
-    dec = O.device_decisions(f.shape[0], want)
+    zero = float(O.kws_forward_int8(O.quantize_input(np.zeros((1, 13, 63))), O.quantize_int8(xiaoa_sd))[0] * 0.125)
+    assert det.cleared_logit() == zero                    # the int8 net on the cleared ring
+    dec = O.device_decisions(f.shape[0], want, cleared_logit=zero)
     assert [(w.end, w.detected) for w in got] == dec
-    np.testing.assert_array_equal(np.asarray([w.logit for w in got], np.float32), want[[e - 62 for e, _ in dec]])
+    np.testing.assert_array_equal(np.asarray([w.logit for w in got if not w.cleared], np.float32),
+                                  want[[w.end - 62 for w in got if not w.cleared]])
 
 
 class _StubModel:
@@ -169,5 +208,6 @@ def test_gpu_device_detector_decisions(gpu):
         got += det.push(f[p:p + 500])
     c = O.device_cmvn(f)
     logits = (c[:, :, 0].astype(np.float32).max(axis=1) / np.float32(2.0) - np.float32(1.0)).astype(np.float32)
-    want = O.device_decisions(f.shape[0], logits)
+    want = O.device_decisions(f.shape[0], logits, cleared_logit=-1.0)   # the stub on the all-zero ring
     assert any(d for _, d in want) and [(w.end, w.detected) for w in got] == want
+    assert any(w.cleared for w in got)
