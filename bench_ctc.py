@@ -4,10 +4,17 @@ B utterances of 3 s (48,000 samples, T = 301 frames at hop 160), synthetic
 (device generator), seeded GRU_CTC_Model weights (the reference ships none),
 fixed V.  One step = log-mel front-end + encoder + 2-layer BiGRU + output
 layer + argmax + greedy decode, inputs resident in HBM and the token
-sequences left there (CTCModel.decode; forward() adds the host list form).  Prints
-one JSON line with utterances/s, the per-stage split, and the torch-CPU
-oracle timed on a bounded sample of the same workload."""
+sequences left there (CTCModel.decode; forward() adds the host list form).
+
+Prints one JSON line: utterances/s over the timed steps, and per stage (HIP
+events on the launch stream, wk_ctc_profile) the mean duration with its
+algorithmic bytes or flops against the MI355X roofline that bounds it, the
+PMC-measured HBM traffic (profiles/ctc_hbm_traffic.json) and which stages are
+library code; `roofline` is the dominant stage's.  The torch-CPU oracle is
+timed on a bounded sample of the same workload as the reported CPU baseline.
+"""
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -15,6 +22,47 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [REPO, os.path.join(REPO, "esp32-wake-word_amd")]
+
+PEAK_HBM_GBS = 8000.0
+PEAK_F16_TFLOPS = 2500.0      # MI355X dense fp16 MFMA
+PEAK_F32_TFLOPS = 157.3
+STAGES = ["logmel", "zscore", "encoder", "proj0", "gru0", "proj1", "gru1", "output", "decode"]
+H, MELS = 128, 80
+
+
+def stage_work(B, T, V, n_samples, f16):
+    """(algorithmic HBM bytes, algorithmic flop) per launch of each stage (the
+    compulsory reads and writes of its inputs and outputs; weights, read once
+    through L2, are counted once)."""
+    rows = B * T
+    a = 2 if f16 else 4                       # activation bytes after the encoder
+    gi = 2 if f16 else 4
+    out = {
+        "logmel": (B * n_samples * 4 + rows * MELS * 4, rows * 4600 + rows * MELS * 2 * 6),
+        "zscore": (2 * rows * MELS * 4, rows * MELS * 5),
+        "encoder": (rows * MELS * 4 + rows * H * a + (H * MELS) * 4, rows * H * MELS * 2),
+        "proj0": (rows * H * a + rows * 6 * H * gi + 6 * H * H * a, rows * 6 * H * H * 2),
+        "gru0": (rows * 6 * H * gi + rows * 2 * H * a, rows * 2 * 3 * H * H * 2),
+        "proj1": (rows * 2 * H * a + rows * 6 * H * gi + 6 * H * 2 * H * a, rows * 6 * H * 2 * H * 2),
+        "gru1": (rows * 6 * H * gi + rows * 2 * H * a, rows * 2 * 3 * H * H * 2),
+        "output": (rows * 2 * H * a + V * 2 * H * a + rows * 4, rows * V * 2 * H * 2),
+        "decode": (2 * rows * 4 + B * 4, 0),
+    }
+    return out
+
+
+def bound_of(stage, f16):
+    return "mfma" if stage == "output" else "hbm"
+
+
+def load_traffic(tag):
+    p = os.path.join(REPO, "profiles", "ctc_hbm_traffic.json")
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+        return d.get(tag, {}), d.get("source")
+    except (OSError, ValueError):
+        return {}, None
 
 
 def main():
@@ -24,54 +72,101 @@ def main():
     ap.add_argument("--seconds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--cpu-utts", type=int, default=8)
+    ap.add_argument("--cpu-utts", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16"],
                     help="GEMM operand precision (config 5 names fp16; fp32 is the parity mode)")
     args = ap.parse_args()
     import torch
     import wakeword
+    from wakeword import _lib
     from oracle import wk_ctc_oracle as CO
 
+    f16 = args.precision == "fp16"
     n = args.seconds * 16000
-    m = CO.make_model(args.vocab, seed=0)
-    g = wakeword.CTCModel(CO.flat_weights(m), args.vocab, precision=args.precision)
-    audio = wakeword.synth_clips(1234, 0, args.batch, n)
+    T = 1 + n // 160
+    B, V = args.batch, args.vocab
+    m = CO.make_model(V, seed=0)
+    g = wakeword.CTCModel(m.state_dict(), V, precision=args.precision)
+    audio = wakeword.synth_clips(1234, 0, B, n)
     for _ in range(args.warmup):
-        g.transcribe(audio, n_samples=n)
+        g.decode(g.features(audio, n_samples=n))
     torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    t_fe = t_all = 0.0
+
+    # timed region: the whole step, host clock, no per-stage events
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ev[0].record()
-        f = g.features(audio, n_samples=n)
-        ev[1].record()
-        g.decode(f)   # tokens + lengths stay in HBM (the host list form is forward())
-        ev[2].record()
-        torch.cuda.synchronize()
-        t_fe += ev[0].elapsed_time(ev[1])
-        t_all += ev[0].elapsed_time(ev[2])
+        tok, ln, _ = g.decode(g.features(audio, n_samples=n))
+    torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    value = args.batch * args.steps / el
+    value = B * args.steps / el
+    assert int(ln.min()) >= 0 and int(ln.max()) <= T
 
-    # CPU baseline: the torch-CPU oracle on a bounded sample
-    x = torch.from_numpy(audio[:args.cpu_utts].cpu().numpy())
-    with torch.no_grad():
-        CO.greedy_decode(m(CO.features(x[:1])))
-        c0 = time.perf_counter()
-        CO.greedy_decode(m(CO.features(x)))
-        cpu = args.cpu_utts / (time.perf_counter() - c0)
-    print(json.dumps({
+    # per-stage durations: the same steps again with HIP events around each stage
+    L = _lib.lib()
+    _lib.check(L.wk_ctc_profile(g._h, 1), "wk_ctc_profile")
+    for _ in range(args.steps):
+        g.decode(g.features(audio, n_samples=n))
+    ms = (C.c_double * len(STAGES))()
+    cnt = (C.c_int64 * len(STAGES))()
+    _lib.check(L.wk_ctc_stage_times(g._h, ms, cnt), "wk_ctc_stage_times")
+    _lib.check(L.wk_ctc_profile(g._h, 0), "wk_ctc_profile")
+    work = stage_work(B, T, V, n, f16)
+    if f16 and cnt[STAGES.index("proj0")] == 0:
+        # projection fused into the recurrence: the layer reads its input rows
+        # instead of the gate inputs and does the projection's flops too
+        rows = B * T
+        for l, din in ((0, H), (1, 2 * H)):
+            by_g, fl_g = work[f"gru{l}"]
+            by_p, fl_p = work[f"proj{l}"]
+            work[f"gru{l}"] = (rows * din * 2 + rows * 2 * H * 2 + 6 * H * din * 2, fl_g + fl_p)
+    traffic, traffic_src = load_traffic(args.precision)
+    kernels = {}
+    for i, s in enumerate(STAGES):
+        if cnt[i] == 0:
+            continue
+        avg = ms[i] / cnt[i]
+        by, fl = work[s]
+        bound = bound_of(s, f16)
+        if bound == "mfma":
+            ach, peak, unit = fl / (avg * 1e-3) / 1e12, PEAK_F16_TFLOPS if f16 else PEAK_F32_TFLOPS, "TFLOP/s"
+        else:
+            ach, peak, unit = by / (avg * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s"
+        kernels[s] = {"ms": round(avg, 4), "bound": bound, "achieved": round(ach, 1), "peak": peak, "unit": unit,
+                      "frac": round(ach / peak, 4), "algorithmic_bytes": by, "algorithmic_flop": fl,
+                      "traffic": traffic.get(s)}
+    lib_stages = ["proj0", "proj1"] + (["output"] if not f16 else [])
+    dom = max(kernels, key=lambda k: kernels[k]["ms"])
+    d = kernels[dom]
+    line = {
         "metric": "CTC utterances/s (3 s @16 kHz, log-mel 80 -> BiGRU x2 H128 -> greedy CTC), config 5",
-        "value": round(value, 1), "unit": "utterances/s", "audio_seconds_per_s": round(value * args.seconds, 1),
-        "batch": args.batch, "vocab": args.vocab, "T": 1 + n // 160, "steps": args.steps,
-        "ms_per_step": round(el / args.steps * 1e3, 3), "frontend_ms": round(t_fe / args.steps, 3),
-        "model_ms": round((t_all - t_fe) / args.steps, 3),
-        "dtype": "f32" if args.precision == "fp32" else "f16 GEMM operands / f32 accumulate + recurrence",
-        "data": "synthetic (device generator), seeded weights",
-        "cpu_baseline": {"value": round(cpu, 2), "unit": "utterances/s", "cores": torch.get_num_threads(),
-                         "kind": "port", "sample": f"{args.cpu_utts} utterances, torch-CPU oracle (oracle/wk_ctc_oracle.py)"},
-    }))
+        "value": round(value, 1), "unit": "utterances/s", "higher_is_better": True,
+        "audio_seconds_per_s": round(value * args.seconds, 1), "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+        "dtype": "f32" if not f16 else "f16 GEMM/MFMA operands, f32 accumulate, f32 gate math and front-end",
+        "data": "synthetic (device generator), seeded GRU_CTC_Model weights (the reference ships none)",
+        "config": {"workload": "config5: CTC head, 3 s utterances", "batch": B, "vocab": V, "T": T,
+                   "precision": args.precision},
+        "roofline": {"kernel": dom, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
+                     "unit": d["unit"], "frac": d["frac"], "traffic": d["traffic"]},
+        "kernels": kernels,
+        "stage_sum_ms": round(sum(k["ms"] for k in kernels.values()), 4),
+        "library_stages": {s: "rocBLAS GEMM (Cijk_*)" for s in lib_stages if s in kernels},
+    }
+    if traffic_src:
+        line["traffic_source"] = traffic_src
+    if not args.no_cpu_baseline:
+        x = torch.from_numpy(audio[:args.cpu_utts].cpu().numpy())
+        with torch.no_grad():
+            CO.greedy_decode(m(CO.features(x[:2])))
+            c0 = time.perf_counter()
+            CO.greedy_decode(m(CO.features(x)))
+            cpu = args.cpu_utts / (time.perf_counter() - c0)
+        line["cpu_baseline"] = {"value": round(cpu, 2), "unit": "utterances/s", "cores": torch.get_num_threads(),
+                                "host_cpus": len(os.sched_getaffinity(0)), "kind": "port",
+                                "sample": f"{args.cpu_utts} utterances of {args.seconds} s in one batch, torch-CPU "
+                                          f"oracle (oracle/wk_ctc_oracle.py: torch.stft log-mel, nn.GRU, V={V})"}
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

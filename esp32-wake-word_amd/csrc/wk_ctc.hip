@@ -757,6 +757,226 @@ __global__ __launch_bounds__(kGru16Threads, 4) void ctc_gru16_kernel(const __hal
 }
 
 // ---------------------------------------------------------------------------
+// fp16 recurrence with the input projection fused in (precision 1, config 5):
+// gi = x W_ih^T is computed inside the persistent recurrence from the layer's
+// input rows x (time-major [T][B][DIN] fp16: the encoder output, or layer 0's
+// [fwd | bwd] outputs), so neither a projection GEMM nor the [rows][768] gate
+// inputs (1.9 GB written and read back per layer at config 5) exist.
+//
+// A workgroup owns 32 utterances (two 16-row tiles) of one direction, one
+// workgroup per CU (8 waves, 2 per SIMD, up to 256 VGPRs each): wave w owns
+// units 16 w .. 16 w + 15 of the r, z and n gates for both row tiles, as in
+// ctc_gru16_kernel.  W_ih of those 48 rows is held as A fragments of
+// v_mfma_f32_16x16x32_f16 (k-steps of 32): k < 128 in VGPRs (48 registers),
+// k >= 128 (layer 1) in an LDS image in fragment order (96 KB per
+// workgroup).  Per step t a wave issues
+//   * the h-part of step t: 2 tiles x 3 gates x 8 MFMAs 16x16x16 on the fp16
+//     state image (accumulating onto the x-part of r and z; n keeps its h-part
+//     apart for r (.)),
+//   * the x-part of step t + 1 (independent of the state, so it fills the
+//     matrix pipe while the h-part chains drain and the gate math runs):
+//     2 tiles x 3 gates x DIN/32 MFMAs 16x16x32 on the staged x tile, the
+//     biases as their initial accumulator (b_ir + b_hr, b_iz + b_hz, b_in),
+// then the fp32 gate math and the new fp16 state, one barrier per step.  The x
+// rows of step t + 2 are staged through a double-buffered LDS tile from a
+// 2-step register ring of cooperative 16-byte loads (rows past B read 0 from
+// the buffer resource's range check); outputs leave as 16-byte pieces of the
+// state image, as in ctc_gru16_kernel.  The gate pre-activations stay in fp32
+// (the GEMM path rounds them to fp16).
+// ---------------------------------------------------------------------------
+constexpr int kGxRows = 32;                       // utterances per workgroup
+constexpr int kGxWaves = 8, kGxThreads = 64 * kGxWaves;
+typedef _Float16 h8x __attribute__((ext_vector_type(8)));
+
+template <int DIN>
+__global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half* __restrict__ x,
+                                                                  const h8x* __restrict__ wih_pk,
+                                                                  const h4* __restrict__ whh_pk,
+                                                                  const float* __restrict__ bih,
+                                                                  const float* __restrict__ bhh, int64_t B, int T,
+                                                                  __half* __restrict__ out) {
+  constexpr int KX = DIN / 32;                 // x-part k-steps
+  constexpr int KXR = KX < 4 ? KX : 4;         // of which in VGPRs (k < 128)
+  constexpr int KXL = KX - KXR;                // in LDS (layer 1: k >= 128)
+  constexpr int XP = DIN + 8;                  // x tile pitch (halves): 16-byte rows, conflict-free B reads
+  constexpr int XCH = kGxRows * DIN / 8;       // 16-byte chunks per x tile
+  constexpr int XPT = (XCH + kGxThreads - 1) / kGxThreads;   // per thread
+  __shared__ __attribute__((aligned(16))) _Float16 h16[2][kGxRows * kH16P];
+  __shared__ __attribute__((aligned(16))) _Float16 xt[2][kGxRows * XP];
+  __shared__ __attribute__((aligned(16))) h8x wl[KXL > 0 ? 3 * kGxWaves * KXL * 64 : 1];
+  __shared__ f32x4 gbias[4][kH / 4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int dir = blockIdx.y;
+  const int n = lane & 15, lg = lane >> 4;
+  const int u0 = 16 * wave + 4 * lg;
+  const int64_t b0 = (int64_t)blockIdx.x * kGxRows;
+  const int nrow = (int)(B - b0 < kGxRows ? B - b0 : kGxRows);
+  const bool live0 = n < nrow, live1 = 16 + n < nrow;
+  // weights: W_hh (16x16x16 A fragments) and W_ih k < 128 (16x16x32) in VGPRs
+  h4 wr[8], wz[8], wn[8];
+  h8x xr[KXR], xz[KXR], xn[KXR];
+  {
+    const h4* p = whh_pk + (size_t)dir * 24 * 8 * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      wr[s] = p[((0 * 8 + wave) * 8 + s) * 64];
+      wz[s] = p[((1 * 8 + wave) * 8 + s) * 64];
+      wn[s] = p[((2 * 8 + wave) * 8 + s) * 64];
+    }
+    const h8x* q = wih_pk + (size_t)dir * 3 * kGxWaves * KX * 64 + lane;   // [dir][gate][wave][ks][lane]
+#pragma unroll
+    for (int s = 0; s < KXR; ++s) {
+      xr[s] = q[((0 * kGxWaves + wave) * KX + s) * 64];
+      xz[s] = q[((1 * kGxWaves + wave) * KX + s) * 64];
+      xn[s] = q[((2 * kGxWaves + wave) * KX + s) * 64];
+    }
+    if constexpr (KXL > 0) {   // k >= 128 -> LDS, [gate][wave][ks - KXR][lane]
+      for (int i = tid; i < 3 * kGxWaves * KXL * 64; i += kGxThreads) {
+        const int l = i & 63, ks = (i >> 6) % KXL, gw = (i >> 6) / KXL;
+        wl[i] = wih_pk[(size_t)dir * 3 * kGxWaves * KX * 64 + ((size_t)gw * KX + KXR + ks) * 64 + l];
+      }
+    }
+  }
+  for (int i = tid; i < kGxRows * kH16P; i += kGxThreads) h16[0][i] = (_Float16)0.0f;
+  if (tid < kH) {
+    const float* bi = bih + dir * 3 * kH;
+    const float* bh = bhh + dir * 3 * kH;
+    float* gbf = reinterpret_cast<float*>(&gbias[0][0]);
+    gbf[tid] = bi[tid] + bh[tid];
+    gbf[kH + tid] = bi[kH + tid] + bh[kH + tid];
+    gbf[2 * kH + tid] = bi[2 * kH + tid];
+    gbf[3 * kH + tid] = bh[2 * kH + tid];
+  }
+  // x rows of a step: 32 adjacent time-major rows, XCH 16-byte chunks, a
+  // register ring kXPf steps deep, then the LDS tile of that step's parity
+  constexpr int kXPf = 2;
+  uint4 xv[kXPf][XPT];
+  auto load_x = [&](int slot, int step) {
+    const int st = step < T ? step : T - 1;
+    const int t = dir == 0 ? st : T - 1 - st;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(x + ((int64_t)t * B + b0) * DIN, (uint32_t)nrow * DIN * 2);
+#pragma unroll
+    for (int c = 0; c < XPT; ++c) {
+      const int ch = tid + c * kGxThreads;
+      xv[slot][c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, ch < XCH ? 16 * ch : 0x40000000, 0, 0));
+    }
+  };
+  auto stage_x = [&](int slot, int buf) {
+#pragma unroll
+    for (int c = 0; c < XPT; ++c) {
+      const int ch = tid + c * kGxThreads;
+      if (ch < XCH) *reinterpret_cast<uint4*>(&xt[buf][(ch / (DIN / 8)) * XP + (ch % (DIN / 8)) * 8]) = xv[slot][c];
+    }
+  };
+  // x-part of one step from the x tile `buf` into g[tile][gate] (bias as the initial accumulator)
+  auto xpart = [&](int buf, f32x4 (&g)[2][3]) {
+    int bq = u0 >> 2;
+    asm volatile("" : "+v"(bq));
+    const f32x4 b_r = gbias[0][bq], b_z = gbias[1][bq], b_n = gbias[2][bq];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      g[q][0] = b_r;
+      g[q][1] = b_z;
+      g[q][2] = b_n;
+    }
+#pragma unroll
+    for (int s = 0; s < KX; ++s) {
+      h8x ar, az, an;
+      if (s < KXR) {
+        ar = xr[s < KXR ? s : 0];
+        az = xz[s < KXR ? s : 0];
+        an = xn[s < KXR ? s : 0];
+      } else {
+        const int sl = s - KXR;
+        ar = wl[((0 * kGxWaves + wave) * (KXL > 0 ? KXL : 1) + sl) * 64 + lane];
+        az = wl[((1 * kGxWaves + wave) * (KXL > 0 ? KXL : 1) + sl) * 64 + lane];
+        an = wl[((2 * kGxWaves + wave) * (KXL > 0 ? KXL : 1) + sl) * 64 + lane];
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const h8x xb = *reinterpret_cast<const h8x*>(&xt[buf][(16 * q + n) * XP + 32 * s + 8 * lg]);
+        g[q][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ar, xb, g[q][0], 0, 0, 0);
+        g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, xb, g[q][1], 0, 0, 0);
+        g[q][2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(an, xb, g[q][2], 0, 0, 0);
+      }
+    }
+  };
+  const int64_t dstep = dir == 0 ? B : -B;   // out is time-major (row t B + b)
+  const int yn = tid >> 4, yc = tid & 15;     // 512 threads = 32 rows x 16 chunks of the state image
+  const bool ylive = yn < nrow;
+  __half* yq = out + ((int64_t)(dir == 0 ? 0 : T - 1) * B + b0 + (ylive ? yn : 0)) * (2 * kH) + dir * kH + 8 * yc;
+  auto store_y = [&](int buf) {
+    if (ylive) *reinterpret_cast<uint4*>(yq) = *reinterpret_cast<const uint4*>(&h16[buf][yn * kH16P + 8 * yc]);
+    yq += dstep * (2 * kH);
+  };
+  // prologue: x_0 and x_1 staged, x_2 / x_3 in the ring, gx of step 0
+  load_x(0, 0);
+  load_x(1, 1);
+  stage_x(0, 0);
+  stage_x(1, 1);
+  load_x(0, 2);
+  load_x(1, 3);
+  __syncthreads();
+  f32x4 ga[2][3], gb[2][3];   // x-parts of the even / odd steps
+  xpart(0, ga);
+  __syncthreads();   // x_0's tile is rewritten (with x_2) during step 0
+  float h[2][4] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+  int cur = 0;
+  auto step_body = [&](int step, f32x4 (&g)[2][3], f32x4 (&gn)[2][3], int slot) {
+    // h-part of this step onto the x-part
+    f32x4 anh[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const _Float16* hb = h16[cur] + (16 * q + n) * kH16P + 4 * lg;
+      h4 hv[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) hv[s] = *reinterpret_cast<const h4*>(hb + 16 * s);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        g[q][0] = __builtin_amdgcn_mfma_f32_16x16x16f16(wr[s], hv[s], g[q][0], 0, 0, 0);
+        g[q][1] = __builtin_amdgcn_mfma_f32_16x16x16f16(wz[s], hv[s], g[q][1], 0, 0, 0);
+        anh[q] = __builtin_amdgcn_mfma_f32_16x16x16f16(wn[s], hv[s], anh[q], 0, 0, 0);
+      }
+    }
+    // x-part of the next step (tile staged during the previous step)
+    if (step + 1 < T) xpart((step + 1) & 1, gn);
+    if (step > 0) store_y(cur);   // the previous step's outputs
+    // x rows of step + 2 into the tile this step's x-part was read from, then refill the ring slot
+    stage_x(slot, step & 1);
+    load_x(slot, step + 2 + kXPf);
+    int bq = u0 >> 2;
+    asm volatile("" : "+v"(bq));
+    const f32x4 bh_c = gbias[3][bq];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const bool live = q == 0 ? live0 : live1;
+      h4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float hn = 0.0f;
+        if (live) {
+          const float r = sigm(g[q][0][i]);
+          const float z = sigm(g[q][1][i]);
+          const float c = tanh_fast(g[q][2][i] + r * (anh[q][i] + bh_c[i]));
+          hn = __builtin_fmaf(z, h[q][i] - c, c);   // (1 - z) c + z h
+        }
+        h[q][i] = hn;
+        o[i] = (_Float16)hn;
+      }
+      *reinterpret_cast<uint2*>(&h16[cur ^ 1][(16 * q + n) * kH16P + u0]) = __builtin_bit_cast(uint2, o);
+    }
+    cur ^= 1;
+    __syncthreads();
+  };
+  for (int step = 0; step < T; step += 2) {
+    step_body(step, ga, gb, 0);
+    if (step + 1 < T) step_body(step + 1, gb, ga, 1);
+  }
+  store_y(cur);   // the last step's outputs
+}
+
+// ---------------------------------------------------------------------------
 // X2c / X3: bias + log_softmax + argmax, one wave per row; greedy collapse
 // ---------------------------------------------------------------------------
 // Online softmax state of one lane: running max (first index on ties, as
@@ -1211,6 +1431,8 @@ struct wk_ctc {
   float* zero_b;        // [V] zeros: the log_softmax kernel's bias in fp16 mode (the logits carry theirs)
   __half* wih16[2];     // fp16 copies (precision 1)
   __half* whh16_pk[2];  // per layer: [2 dir][24 tiles][8 k-steps][64 lanes][4]
+  __half* wih16x_pk[2]; // per layer: [2 dir][3 gates][8 waves][din/32 k-steps][64 lanes][8] (fused-projection GRU)
+  bool gru_gemm;        // fp16 mode: input projections as a separate GEMM (WAKEWORD_CTC_GEMM=1; A/B and checks)
   __half* out_w16;
   float* fft_win;       // [400] periodic Hann
   float* fft_tw;        // [20 k1][20 n2] W400^(n2 k1), complex
@@ -1224,6 +1446,13 @@ struct wk_ctc {
   int* best;
   int64_t last_batch;   // geometry of the last wk_ctc_forward (wk_ctc_frame_argmax)
   int32_t last_T;
+  // stage timing (wk_ctc_profile): events recorded around each stage on the
+  // call's stream, folded into per-stage sums when read or when the ring fills
+  int prof;
+  struct { int stage; hipEvent_t a, b; } ev[64];
+  int n_ev;
+  double stage_ms[WK_CTC_N_STAGES];
+  int64_t stage_n[WK_CTC_N_STAGES];
 };
 
 namespace {
@@ -1244,11 +1473,52 @@ void free_ws(wk_ctc* c) {
   c->ws_rows = 0;
 }
 
+// Fold the recorded stage events into the per-stage sums (synchronises on them).
+hipError_t fold_events(wk_ctc* c) {
+  hipError_t err = hipSuccess;
+  for (int i = 0; i < c->n_ev; ++i) {
+    float ms = 0.0f;
+    hipError_t e = hipEventSynchronize(c->ev[i].b);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->ev[i].a, c->ev[i].b);
+    if (e == hipSuccess) {
+      c->stage_ms[c->ev[i].stage] += ms;
+      c->stage_n[c->ev[i].stage] += 1;
+    } else if (err == hipSuccess) {
+      err = e;
+    }
+    (void)hipEventDestroy(c->ev[i].a);
+    (void)hipEventDestroy(c->ev[i].b);
+  }
+  c->n_ev = 0;
+  return err;
+}
+
+// Stage bracket: records an event pair around `launch` when profiling is on.
+template <typename F>
+wk_status timed(wk_ctc* c, int stage, hipStream_t st, F launch) {
+  if (!c->prof) return launch();
+  if (c->n_ev == 64 && fold_events(c) != hipSuccess) return fail(WK_ERR_HIP, "wk_ctc stage timing");
+  auto& e = c->ev[c->n_ev];
+  if (hipEventCreate(&e.a) != hipSuccess) return fail(WK_ERR_HIP, "hipEventCreate");
+  if (hipEventCreate(&e.b) != hipSuccess) {
+    (void)hipEventDestroy(e.a);
+    return fail(WK_ERR_HIP, "hipEventCreate");
+  }
+  e.stage = stage;
+  ++c->n_ev;
+  (void)hipEventRecord(e.a, st);
+  const wk_status s = launch();
+  (void)hipEventRecord(e.b, st);
+  return s;
+}
+
 void free_all(wk_ctc* c) {
+  (void)fold_events(c);
   free_ws(c);
   void* ps[] = {c->enc_w, c->enc_b, c->ln_g, c->ln_b, c->wih[0], c->wih[1], c->bih[0], c->bih[1], c->bhh[0],
                 c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->zero_b, c->fb_w, c->wih16[0], c->wih16[1],
-                c->out_w16, c->fft_win, c->fft_tw, c->fb_start, c->fb_len, c->fb_off, c->whh16_pk[0], c->whh16_pk[1]};
+                c->out_w16, c->fft_win, c->fft_tw, c->fb_start, c->fb_len, c->fb_off, c->whh16_pk[0], c->whh16_pk[1],
+                c->wih16x_pk[0], c->wih16x_pk[1]};
   for (void* q : ps) (void)hipFree(q);
   if (c->blas) rocblas_destroy_handle(c->blas);
 }
@@ -1297,6 +1567,8 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     if (!c) return WK_ERR_NO_MEMORY;
     c->cfg = *cfg;
     c->f16 = cfg->precision == 1;
+    const char* gg = getenv("WAKEWORD_CTC_GEMM");
+    c->gru_gemm = gg && gg[0] == '1';
     hipDeviceProp_t prop;
     c->n_cu = hipGetDeviceProperties(&prop, cfg->device) == hipSuccess ? prop.multiProcessorCount : 256;
     if (rocblas_create_handle(&c->blas) != rocblas_status_success) {
@@ -1339,6 +1611,19 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
       }
       e = upload(&c->wih[l], wih.data(), wih.size());
       if (e == hipSuccess && c->f16) e = upload_f16(&c->wih16[l], wih.data(), wih.size());
+      if (e == hipSuccess && c->f16) {   // W_ih as 16x16x32 A fragments: [dir][gate][wave][ks][lane][8]
+        const int kx = din / 32;
+        std::vector<float> px((size_t)2 * 3 * 8 * kx * 64 * 8);
+        size_t o = 0;
+        for (int d = 0; d < 2; ++d)
+          for (int g = 0; g < 3; ++g)
+            for (int w = 0; w < 8; ++w)
+              for (int ks = 0; ks < kx; ++ks)
+                for (int ln = 0; ln < 64; ++ln)
+                  for (int j = 0; j < 8; ++j)
+                    px[o++] = wih[((size_t)d * 3 * H + g * H + 16 * w + (ln & 15)) * din + 32 * ks + 8 * (ln >> 4) + j];
+        e = upload_f16(&c->wih16x_pk[l], px.data(), px.size());
+      }
       if (e == hipSuccess) e = upload(&c->bih[l], bih.data(), bih.size());
       if (e == hipSuccess) e = upload(&c->bhh[l], bhh.data(), bhh.size());
       if (e == hipSuccess) e = upload(&c->whh_pk[l], pk.data(), pk.size());
@@ -1424,10 +1709,18 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
     // n_valid == 0: every sample is padding; the kernel's (masked) loads then
     // read a device table instead of a possibly empty audio buffer
     const float* au = nv > 0 ? d_audio : c->fft_win;
-    hipLaunchKernelGGL(ctc_logmel_fft_kernel, dim3((unsigned)(blocks < 8 * c->n_cu ? blocks : 8 * c->n_cu)), dim3(256), 0,
-                       st, au, nv > 0 ? stride : (int64_t)0, nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->fb_start, c->fb_len,
-                       c->fb_off, c->fb_w, c->n_fbw, d_feats);
-    hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
+    wk_status s = timed(c, WK_CTC_STAGE_LOGMEL, st, [&]() -> wk_status {
+      hipLaunchKernelGGL(ctc_logmel_fft_kernel, dim3((unsigned)(blocks < 8 * c->n_cu ? blocks : 8 * c->n_cu)), dim3(256),
+                         0, st, au, nv > 0 ? stride : (int64_t)0, nv, n_samples, T, rows, c->fft_win, c->fft_tw,
+                         c->fb_start, c->fb_len, c->fb_off, c->fb_w, c->n_fbw, d_feats);
+      return WK_OK;
+    });
+    if (s == WK_OK)
+      s = timed(c, WK_CTC_STAGE_ZSCORE, st, [&]() -> wk_status {
+        hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
+        return WK_OK;
+      });
+    if (s != WK_OK) return s;
     e = hipGetLastError();
     return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_features launch");
   });
@@ -1449,7 +1742,7 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
       if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
       free_ws(c);
       if ((!f16 && (e = hipMalloc(&c->x0, sizeof(float) * rows * H)) != hipSuccess) ||
-          (e = hipMalloc(&c->gi, sizeof(float) * rows * 6 * H)) != hipSuccess ||
+          ((!f16 || c->gru_gemm) && (e = hipMalloc(&c->gi, sizeof(float) * rows * 6 * H)) != hipSuccess) ||
           (!f16 && (e = hipMalloc(&c->y0, sizeof(float) * rows * 2 * H)) != hipSuccess) ||
           (!f16 && (e = hipMalloc(&c->y1, sizeof(float) * rows * 2 * H)) != hipSuccess) ||
           (!f16 && (e = hipMalloc(&c->logits, sizeof(float) * rows * V)) != hipSuccess) ||
@@ -1467,62 +1760,128 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
     c->last_batch = batch;
     c->last_T = T;
     const int enc_grid = (int)((rows + 63) / 64 < 8 * c->n_cu ? (rows + 63) / 64 : 8 * c->n_cu);
-    if (f16)
-      hipLaunchKernelGGL(ctc_encoder16_kernel, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w, c->enc_b,
-                         c->ln_g, c->ln_b, (int)batch, T, c->x0h);   // fp16 path: time-major rows from here on
-    else
-      hipLaunchKernelGGL(ctc_encoder_kernel<float>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
-                         c->enc_b, c->ln_g, c->ln_b, c->x0);
+    wk_status s = timed(c, WK_CTC_STAGE_ENCODER, st, [&]() -> wk_status {
+      if (f16)
+        hipLaunchKernelGGL(ctc_encoder16_kernel, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w, c->enc_b,
+                           c->ln_g, c->ln_b, (int)batch, T, c->x0h);   // fp16 path: time-major rows from here on
+      else
+        hipLaunchKernelGGL(ctc_encoder_kernel<float>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
+                           c->enc_b, c->ln_g, c->ln_b, c->x0);
+      return WK_OK;
+    });
+    if (s != WK_OK) return s;
     const float* in = c->x0;
     const __half* in16 = c->x0h;
     float* ys[2] = {c->y0, c->y1};
     __half* ys16[2] = {c->y0h, c->y1h};
     for (int l = 0; l < 2; ++l) {
       const int din = l == 0 ? H : 2 * H;
-      wk_status s = f16 ? gemm_nt(c->blas, rows, 6 * H, din, in16, c->wih16[l], c->gi, true, true)   // fp16 gates
-                        : gemm_nt(c->blas, rows, 6 * H, din, in, c->wih[l], c->gi, false);
+      if (f16 && !c->gru_gemm) {   // projection fused into the recurrence: no GEMM, no gate-input tensor
+        const dim3 gx((unsigned)((batch + kGxRows - 1) / kGxRows), 2);
+        s = timed(c, WK_CTC_STAGE_GRU0 + 2 * l, st, [&]() -> wk_status {
+          if (l == 0)
+            hipLaunchKernelGGL(ctc_gru16x_kernel<128>, gx, dim3(kGxThreads), 0, st, in16, (const h8x*)c->wih16x_pk[0],
+                               (const h4*)c->whh16_pk[0], c->bih[0], c->bhh[0], batch, T, ys16[0]);
+          else
+            hipLaunchKernelGGL(ctc_gru16x_kernel<256>, gx, dim3(kGxThreads), 0, st, in16, (const h8x*)c->wih16x_pk[1],
+                               (const h4*)c->whh16_pk[1], c->bih[1], c->bhh[1], batch, T, ys16[1]);
+          return WK_OK;
+        });
+        if (s != WK_OK) return s;
+        in16 = ys16[l];
+        continue;
+      }
+      s = timed(c, WK_CTC_STAGE_PROJ0 + 2 * l, st, [&]() -> wk_status {
+        return f16 ? gemm_nt(c->blas, rows, 6 * H, din, in16, c->wih16[l], c->gi, true, true)   // fp16 gates
+                   : gemm_nt(c->blas, rows, 6 * H, din, in, c->wih[l], c->gi, false);
+      });
       if (s != WK_OK) return s;
       const dim3 gg((unsigned)((batch + kGruBatch - 1) / kGruBatch), 2);
-      if (f16)
-        hipLaunchKernelGGL(ctc_gru16_kernel, gg, dim3(kGru16Threads), 0, st, (const __half*)c->gi, (const h4*)c->whh16_pk[l], c->bih[l],
-                           c->bhh[l], batch, T, ys16[l]);
-      else
-        hipLaunchKernelGGL(ctc_gru_kernel, gg, dim3(kGruThreads), 0, st, c->gi, c->whh_pk[l], c->bih[l], c->bhh[l],
-                           batch, T, ys[l]);
+      s = timed(c, WK_CTC_STAGE_GRU0 + 2 * l, st, [&]() -> wk_status {
+        if (f16)
+          hipLaunchKernelGGL(ctc_gru16_kernel, gg, dim3(kGru16Threads), 0, st, (const __half*)c->gi,
+                             (const h4*)c->whh16_pk[l], c->bih[l], c->bhh[l], batch, T, ys16[l]);
+        else
+          hipLaunchKernelGGL(ctc_gru_kernel, gg, dim3(kGruThreads), 0, st, c->gi, c->whh_pk[l], c->bih[l], c->bhh[l],
+                             batch, T, ys[l]);
+        return WK_OK;
+      });
+      if (s != WK_OK) return s;
       in = ys[l];
       in16 = ys16[l];
     }
     if (f16) {
       // fused output layer + argmax; fp16 logits are written only for log_softmax
       const dim3 og((unsigned)((rows + out_rows(d_log_probs != nullptr) - 1) / out_rows(d_log_probs != nullptr)));
-      if (d_log_probs) {
-        hipLaunchKernelGGL(ctc_out_argmax16_kernel<true>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
-                           c->out_b, rows, V, c->logits16, c->best);
-        hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits16,
-                           c->zero_b, rows, V, d_log_probs, (int*)nullptr, (int)batch, T);   // bias already in
-      } else {
-        hipLaunchKernelGGL(ctc_out_argmax16_kernel<false>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
-                           c->out_b, rows, V, (__half*)nullptr, c->best);
-      }
-      hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
-                         d_tokens, d_lengths, 1);
+      s = timed(c, WK_CTC_STAGE_OUTPUT, st, [&]() -> wk_status {
+        if (d_log_probs) {
+          hipLaunchKernelGGL(ctc_out_argmax16_kernel<true>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
+                             c->out_b, rows, V, c->logits16, c->best);
+          hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st,
+                             c->logits16, c->zero_b, rows, V, d_log_probs, (int*)nullptr, (int)batch, T);   // bias already in
+        } else {
+          hipLaunchKernelGGL(ctc_out_argmax16_kernel<false>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
+                             c->out_b, rows, V, (__half*)nullptr, c->best);
+        }
+        return WK_OK;
+      });
+      if (s == WK_OK)
+        s = timed(c, WK_CTC_STAGE_DECODE, st, [&]() -> wk_status {
+          hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
+                             d_tokens, d_lengths, 1);
+          return WK_OK;
+        });
+      if (s != WK_OK) return s;
       e = hipGetLastError();
       return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_forward launch");
     }
-    wk_status s = gemm_nt(c->blas, rows, V, 2 * H, c->y1, c->out_w, c->logits, false);
-    if (s != WK_OK) return s;
     const bool arg_only = !d_log_probs && V % Vec<float>::N == 0 && V / Vec<float>::N <= 64 * kArgChunks && V <= 16384;
     const unsigned ag = (unsigned)((rows + 3) / 4 < 8 * c->n_cu ? (rows + 3) / 4 : 8 * c->n_cu);
-    if (arg_only)
-      hipLaunchKernelGGL(ctc_argmax_only_kernel<float>, dim3(ag), dim3(256), V * sizeof(float), st, c->logits,
-                         c->out_b, rows, V, c->best);
-    else
-      hipLaunchKernelGGL(ctc_argmax_kernel<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits,
-                         c->out_b, rows, V, d_log_probs, c->best);
-    hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
-                       d_tokens, d_lengths);
+    s = timed(c, WK_CTC_STAGE_OUTPUT, st, [&]() -> wk_status {
+      wk_status g = gemm_nt(c->blas, rows, V, 2 * H, c->y1, c->out_w, c->logits, false);
+      if (g != WK_OK) return g;
+      if (arg_only)
+        hipLaunchKernelGGL(ctc_argmax_only_kernel<float>, dim3(ag), dim3(256), V * sizeof(float), st, c->logits,
+                           c->out_b, rows, V, c->best);
+      else
+        hipLaunchKernelGGL(ctc_argmax_kernel<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, c->logits,
+                           c->out_b, rows, V, d_log_probs, c->best);
+      return WK_OK;
+    });
+    if (s == WK_OK)
+      s = timed(c, WK_CTC_STAGE_DECODE, st, [&]() -> wk_status {
+        hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
+                           d_tokens, d_lengths);
+        return WK_OK;
+      });
+    if (s != WK_OK) return s;
     e = hipGetLastError();
     return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_forward launch");
+  });
+}
+
+wk_status wk_ctc_profile(wk_ctc* c, int32_t enable) {
+  if (!c) return invalid("wk_ctc_profile: null handle");
+  return on_device(c->cfg.device, [&]() -> wk_status {
+    const hipError_t e = fold_events(c);
+    for (int i = 0; i < WK_CTC_N_STAGES; ++i) {
+      c->stage_ms[i] = 0.0;
+      c->stage_n[i] = 0;
+    }
+    c->prof = enable ? 1 : 0;
+    return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_profile");
+  });
+}
+
+wk_status wk_ctc_stage_times(wk_ctc* c, double* ms_sum, int64_t* counts) {
+  if (!c || !ms_sum || !counts) return invalid("wk_ctc_stage_times: null argument");
+  return on_device(c->cfg.device, [&]() -> wk_status {
+    const hipError_t e = fold_events(c);
+    for (int i = 0; i < WK_CTC_N_STAGES; ++i) {
+      ms_sum[i] = c->stage_ms[i];
+      counts[i] = c->stage_n[i];
+    }
+    return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_stage_times");
   });
 }
 

@@ -30,7 +30,8 @@ EXPORTS = ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_syn
            "analyze_mfcc_range", "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push",
            "wk_ctc_num_weights", "wk_ctc_create", "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward",
            "wk_wav_read", "wk_wav_load_batch", "wk_augment", "flow_extract_mfcc_single_frame", "wk_device_cmvn",
-           "wk_check_device_errors", "wk_ctc_frame_argmax", "wk_record_front", "wk_quantize_frames")
+           "wk_check_device_errors", "wk_ctc_frame_argmax", "wk_record_front", "wk_quantize_frames",
+           "wk_ctc_profile", "wk_ctc_stage_times")
 
 
 class WkConfig(C.Structure):
@@ -88,6 +89,8 @@ def _declare(L):
     L.wk_ctc_frame_argmax.argtypes = [vp, i64, i32, vp, vp]
     L.wk_record_front.argtypes = [vp, i64, vp, vp, vp]
     L.wk_quantize_frames.argtypes = [vp, i64, vp, vp]
+    L.wk_ctc_profile.argtypes = [vp, i32]
+    L.wk_ctc_stage_times.argtypes = [vp, vp, vp]
     L.wk_wav_read.argtypes = [C.c_char_p, vp, i32, C.POINTER(WkWavInfo)]
     L.wk_wav_load_batch.argtypes = [C.POINTER(C.c_char_p), i32, i32, C.c_float, u32, vp, vp]
     L.wk_augment.argtypes = [vp, i32, C.c_float, C.c_float, C.c_float, u32, vp, i32]
@@ -97,7 +100,7 @@ def _declare(L):
                  "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push", "wk_ctc_create",
                  "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward", "wk_wav_read", "wk_wav_load_batch",
                  "wk_augment", "wk_device_cmvn", "wk_ctc_frame_argmax", "wk_record_front",
-                 "wk_quantize_frames"):
+                 "wk_quantize_frames", "wk_ctc_profile", "wk_ctc_stage_times"):
         getattr(L, name).restype = i32
 
 

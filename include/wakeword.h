@@ -228,6 +228,26 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
 wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T, float* d_log_probs_or_null,
                          int32_t* d_tokens, int32_t* d_lengths, void* stream);
 
+/* Stage timing for measurement (bench_ctc.py): while enabled, every stage of
+ * wk_ctc_features / wk_ctc_forward is bracketed by a pair of HIP events on the
+ * call's stream; wk_ctc_stage_times synchronises on them and returns, per
+ * stage, the summed milliseconds and the number of timed launches since the
+ * last wk_ctc_profile call (which clears them).  Off by default (no events). */
+enum {
+  WK_CTC_STAGE_LOGMEL = 0,  /* X1 log-mel (framing, FFT, power, mel, ln)            */
+  WK_CTC_STAGE_ZSCORE,      /* X1 global z-score                                    */
+  WK_CTC_STAGE_ENCODER,     /* Linear 80->128 + LayerNorm + ReLU                    */
+  WK_CTC_STAGE_PROJ0,       /* GRU layer 0 input projection (x W_ih^T, both dirs)   */
+  WK_CTC_STAGE_GRU0,        /* GRU layer 0 recurrence (both directions)             */
+  WK_CTC_STAGE_PROJ1,       /* GRU layer 1 input projection                         */
+  WK_CTC_STAGE_GRU1,        /* GRU layer 1 recurrence                               */
+  WK_CTC_STAGE_OUTPUT,      /* output layer + argmax (+ log_softmax when requested) */
+  WK_CTC_STAGE_DECODE,      /* greedy CTC collapse                                  */
+  WK_CTC_N_STAGES
+};
+wk_status wk_ctc_profile(wk_ctc* c, int32_t enable);
+wk_status wk_ctc_stage_times(wk_ctc* c, double* ms_sum /* [WK_CTC_N_STAGES] */, int64_t* counts /* [WK_CTC_N_STAGES] */);
+
 /* X3's per-frame argmax -- decode_predictions' `predictions` (ctc.py:454,
  * first maximum per frame), the frame tokens the greedy decode collapsed --
  * of the handle's last wk_ctc_forward: d_pred [batch][T] int32.  batch and T

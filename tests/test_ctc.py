@@ -263,3 +263,34 @@ def test_ctc_decode_predictions_text_round_trip():
     seqs = CO.greedy_decode(lp2)
     assert decode_predictions(lp2, idx_to_char) == tokens_to_text(seqs, idx_to_char)
     assert any("<unk>" in s for s in decode_predictions(lp2, idx_to_char))   # ids past the map
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 33, 200])
+def test_ctc_fp16_fused_projection_matches_gemm_path(B, monkeypatch):
+    """fp16 mode computes the GRU input projections inside the recurrence (no
+    projection GEMM, fp32 gate pre-activations); WAKEWORD_CTC_GEMM=1 keeps the
+    separate GEMM (fp16 gate pre-activations).  Both track the oracle within
+    the fp16 bound and agree with each other on confident frames; ragged B
+    (workgroups own 32 utterances) included."""
+    import wakeword
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    m = CO.make_model(V, seed=13)
+    g_fused = wakeword.CTCModel(m.state_dict(), V, precision="fp16")
+    monkeypatch.setenv("WAKEWORD_CTC_GEMM", "1")
+    g_gemm = wakeword.CTCModel(m.state_dict(), V, precision="fp16")
+    monkeypatch.delenv("WAKEWORD_CTC_GEMM")
+    feats = CO.features(torch.from_numpy(O.synth_clips(19, 0, B, 48000)))
+    with torch.no_grad():
+        ref_lp = m(feats)
+    _, lp_f = g_fused.forward(feats, return_log_probs=True)
+    _, lp_g = g_gemm.forward(feats, return_log_probs=True)
+    lp_f, lp_g = lp_f.cpu(), lp_g.cpu()
+    assert np.abs((lp_f - ref_lp).numpy()).max() <= 0.05
+    assert np.abs((lp_g - ref_lp).numpy()).max() <= 0.05
+    top2 = torch.topk(ref_lp, 2, dim=-1).values
+    ok = (top2[..., 0] - top2[..., 1]) > 0.2
+    assert (lp_f.argmax(-1) == ref_lp.argmax(-1))[ok].all()
+    # fp32 gate pre-activations: the fused path is at least as close to the oracle
+    assert np.abs((lp_f - ref_lp).numpy()).mean() <= np.abs((lp_g - ref_lp).numpy()).mean() * 1.05
