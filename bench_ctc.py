@@ -51,8 +51,9 @@ def stage_work(B, T, V, n_samples, f16):
     return out
 
 
-def bound_of(stage, f16):
-    return "mfma" if stage == "output" else "hbm"
+def bound_of(stage, f16, fused=False):
+    # the fused recurrence does the projection's MFMA work too: priced on the matrix cores
+    return "mfma" if stage == "output" or (fused and stage in ("gru0", "gru1")) else "hbm"
 
 
 def load_traffic(tag):
@@ -112,7 +113,8 @@ def main():
     _lib.check(L.wk_ctc_stage_times(g._h, ms, cnt), "wk_ctc_stage_times")
     _lib.check(L.wk_ctc_profile(g._h, 0), "wk_ctc_profile")
     work = stage_work(B, T, V, n, f16)
-    if f16 and cnt[STAGES.index("proj0")] == 0:
+    fused = f16 and cnt[STAGES.index("proj0")] == 0
+    if fused:
         # projection fused into the recurrence: the layer reads its input rows
         # instead of the gate inputs and does the projection's flops too
         rows = B * T
@@ -127,7 +129,7 @@ def main():
             continue
         avg = ms[i] / cnt[i]
         by, fl = work[s]
-        bound = bound_of(s, f16)
+        bound = bound_of(s, f16, fused)
         if bound == "mfma":
             ach, peak, unit = fl / (avg * 1e-3) / 1e12, PEAK_F16_TFLOPS if f16 else PEAK_F32_TFLOPS, "TFLOP/s"
         else:
