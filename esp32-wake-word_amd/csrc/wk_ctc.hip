@@ -250,6 +250,205 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// X1, two frames per complex FFT (round 3).  The 400-point DFT of a real frame
+// wastes half of a complex FFT, so a lane group runs one complex four-step FFT
+// on z = x_a + i x_b of two frames and separates the spectra afterwards:
+// X_a[k] = (Z[k] + conj Z[400-k]) / 2, X_b[k] = (Z[k] - conj Z[400-k]) / (2i).
+// Lane (g = lane / 20, q = lane % 20) of a wave owns frame pair g (rows
+// 6 ps + 2 g, + 1; lanes 60-63 idle):
+//   stage 1: lane (g, n2 = q): DFT-20 over n1 of z[20 n1 + n2] -> A[n2][k1],
+//            all 20 k1 (no conjugate symmetry for a complex input);
+//   stage 2: lane (g, k1 = q): twiddle W400^(n2 k1), DFT-20 over n2 ->
+//            Z[k1 + 20 k2] in v[k2];
+//   exchange: the partner of bin k1 + 20 k2 is 400 - k1 - 20 k2 =
+//            (20 - k1) + 20 (19 - k2) in lane 20 - k1 (k1 > 0), or
+//            20 (20 - k2) in the lane itself (k1 = 0): every lane publishes
+//            v[10..19] (lane 0 also v[0]) and reads its partner's, one LDS
+//            round trip;
+//   power:   |Z[k] + conj Z'|^2 and |Z[k] - conj Z'|^2 for k = q + 20 k2,
+//            k2 = 0..9 (bin 200 by lane 0), stored as {P_a, P_b} pairs; the
+//            1/4 of the separation rides in the mel weights (exact);
+//   mel:     straight-line per-lane windows (weights in registers), one
+//            8-byte read per pair and tap feeding two FMAs, then ln(+1e-8).
+// One 12-wave workgroup per CU (3 waves per SIMD), the tables once per CU.
+// LDS pitches (see the per-access notes) keep the stage-1 writes, stage-2
+// reads and pair-power writes free of bank conflicts.
+// ---------------------------------------------------------------------------
+constexpr int kF2Waves = 12, kF2Pairs = 3;
+constexpr int kMelW1 = 8, kMelW2 = 7;   // mel windows: mels 0-63 <= 8 bins, mels 64-79 <= 14 = 2 x 7 (host-checked)
+constexpr int kA2Pitch = 25;    // A[g][n2][k1] rows (float2): 25 = 1 mod 8 -> stage-2 lane groups start 40 banks apart
+constexpr int kE2Pitch = 12;    // exchange rows (float2), 16-byte aligned for the b128 writes
+constexpr int kP2Pitch = 212;   // pair-power rows (float2): 2 x 212 = 40 mod 64 banks between lane groups
+static_assert(kF2Pairs * kP2Pitch <= kF2Pairs * 20 * kA2Pitch, "power rows alias the A region");
+static_assert(kF2Pairs * 20 * kE2Pitch <= kF2Pairs * 20 * kA2Pitch, "exchange rows alias the A region");
+struct CtcFft2Lds {
+  float win[kNfft];
+  f2 tw[20][kTwPitch];
+  f2 w[kF2Waves][kF2Pairs * 20 * kA2Pitch];   // per wave: A, then the exchange, then the power rows
+};
+
+__global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const float* __restrict__ audio, int64_t stride,
+                                                                            int n_valid, int n_pad, int T, int64_t rows,
+                                                                            const float* __restrict__ win_g,
+                                                                            const float* __restrict__ tw_g,
+                                                                            const float* __restrict__ melw,
+                                                                            const int* __restrict__ melws,
+                                                                            float* __restrict__ feats) {
+  __shared__ CtcFft2Lds L;
+  constexpr int NT = kF2Waves * 64;
+  for (int i = threadIdx.x; i < kNfft; i += NT) L.win[i] = win_g[i];
+  for (int i = threadIdx.x; i < 400; i += NT) L.tw[i / 20][i % 20] = f2{tw_g[2 * i], tw_g[2 * i + 1]};
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane / 20, q = lane - 20 * (lane / 20);   // pair slot (3 = idle lanes 60-63), n2 / k1
+  f2* A = L.w[wv];
+  constexpr int kRowsPerPass = 2 * kF2Pairs;
+  const int64_t passes = (rows + kRowsPerPass - 1) / kRowsPerPass;
+  const int64_t pstep = (int64_t)gridDim.x * kF2Waves;
+  const int nv_min = n_valid < n_pad ? n_valid : n_pad;
+  // The lane's 20 samples x[20 n1 + q] of one frame (row) of pass ps_; idle
+  // lanes and rows past the end read utterance 0's first samples (nothing
+  // they compute is stored).  Wave-uniform paths, exactly 20 loads each.
+  auto load_raw = [&](int64_t ps_, int fo, float (&raw)[20]) {
+    const int64_t row = ps_ * kRowsPerPass + 2 * g + fo;
+    const bool live = g < kF2Pairs && ps_ < passes && row < rows;
+    const int rr = live ? (int)row : 0;   // rows < 2^31 (host check)
+    const int b = (int)((unsigned)rr / (unsigned)T), t = rr - b * T;
+    const float* xa = audio + (int64_t)b * stride;
+    const int p0 = live ? t * kHop - kNfft / 2 : 0;
+    if (__all(p0 >= 0 && p0 + kNfft <= nv_min)) {
+      const float* xp = xa + p0 + q;
+#pragma unroll
+      for (int n1 = 0; n1 < 20; ++n1) raw[n1] = xp[20 * n1];
+    } else {
+#pragma unroll
+      for (int n1 = 0; n1 < 20; ++n1) {
+        int p = p0 + 20 * n1 + q;
+        p = p < 0 ? -p : p;
+        p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
+        const bool in = p < n_valid;
+        const float x = xa[in ? p : 0];
+        raw[n1] = in ? x : 0.0f;
+      }
+    }
+  };
+  // the lane's mel windows: mel `lane` (kMelW1 taps from bin ws1) and half
+  // `lane & 1` of mel 64 + lane / 2 (kMelW2 taps from ws2; lanes >= 32: zero weights)
+  float mw1[kMelW1], mw2[kMelW2];
+#pragma unroll
+  for (int j = 0; j < kMelW1; ++j) mw1[j] = melw[lane * kMelW1 + j];
+#pragma unroll
+  for (int j = 0; j < kMelW2; ++j) mw2[j] = melw[64 * kMelW1 + lane * kMelW2 + j];
+  const int ws1 = melws[lane], ws2 = melws[64 + lane];
+  float ra[20], rb[20];
+  load_raw((int64_t)blockIdx.x * kF2Waves + wv, 0, ra);
+  load_raw((int64_t)blockIdx.x * kF2Waves + wv, 1, rb);
+  const bool lact = g < kF2Pairs;
+  for (int64_t ps = (int64_t)blockIdx.x * kF2Waves + wv; ps < passes; ps += pstep) {
+    // stage 1: lane (g, n2 = q): DFT-20 over n1 of z[20 n1 + n2] = w (x_a + i x_b)
+    f2 v[20];
+#pragma unroll
+    for (int n1 = 0; n1 < 20; ++n1) {
+      const float wn = L.win[20 * n1 + q];
+      v[n1] = f2{ra[n1], rb[n1]} * f2{wn, wn};
+      asm volatile("" ::"v"(v[n1].x), "v"(v[n1].y) : "memory");   // ahead of the next pass's loads
+    }
+    load_raw(ps + pstep, 0, ra);
+    load_raw(ps + pstep, 1, rb);
+    dft20(v);
+    // A rows: lane (g, q) writes A[g][q][0..19]; pitch 25 float2 = 50 dwords:
+    // 50 i mod 64 over 32 lanes is 2 x (25 i mod 32), all distinct
+    if (lact) {
+#pragma unroll
+      for (int k1 = 0; k1 < 20; ++k1) A[(g * 20 + q) * kA2Pitch + k1] = v[k1];
+    }
+    wave_lds_sync();
+    // stage 2: lane (g, k1 = q) gathers column k1: lane groups g start at
+    // 40 g x 25 = 40 g mod 64 dwords, so half-waves touch disjoint banks
+    if (lact) {
+#pragma unroll
+      for (int n2 = 0; n2 < 20; ++n2) v[n2] = cmul2(A[(g * 20 + n2) * kA2Pitch + q], L.tw[q][n2]);
+    }
+    dft20(v);   // Z[q + 20 k2] in v[k2]
+    // exchange (the A reads of this wave are done: one wave's LDS ops complete in order)
+    f2* E = A;
+    if (lact) {
+      f2* e = E + (g * 20 + q) * kE2Pitch;
+#pragma unroll
+      for (int j = 0; j < 10; j += 2) *reinterpret_cast<f32x4*>(e + j) = f32x4{v[10 + j].x, v[10 + j].y, v[11 + j].x, v[11 + j].y};
+      if (q == 0) e[10] = v[0];
+    }
+    wave_lds_sync();
+    // partner values pp[k2] = Z[400 - q - 20 k2]: lane 20 - q's v[19 - k2]
+    // (= its published slot 9 - k2), or for q = 0 the lane's own v[20 - k2]
+    // (slots shifted by one, slot 10 = v[0])
+    f2 pp[10];
+    {
+      const f2* base = E + (g * 20 + (q == 0 ? 0 : 20 - q)) * kE2Pitch + (q == 0 ? 1 : 0);
+#pragma unroll
+      for (int k2 = 0; k2 < 10; ++k2) pp[k2] = base[9 - k2];
+    }
+    wave_lds_sync();
+    // pair powers {|Z + conj Z'|^2, |Z - conj Z'|^2} = 4 {P_a, P_b}; row pitch
+    // 212 float2: lane groups 40 banks apart, conflict-free 8-byte writes
+    f2* PW = A;
+    if (lact) {
+      f2* pr = PW + g * kP2Pitch + q;
+#pragma unroll
+      for (int k2 = 0; k2 < 10; ++k2) {
+        const f2 sa = f2{v[k2].x + pp[k2].x, v[k2].y - pp[k2].y};   // Z + conj Z'
+        const f2 sb = f2{v[k2].x - pp[k2].x, v[k2].y + pp[k2].y};   // Z - conj Z'
+        pr[20 * k2] = f2{__builtin_fmaf(sa.x, sa.x, sa.y * sa.y), __builtin_fmaf(sb.x, sb.x, sb.y * sb.y)};
+      }
+      if (q == 0) {   // bin 200 is its own partner: 4 {Re^2, Im^2}
+        const f2 z = v[10];
+        pr[200] = f2{4.0f * z.x * z.x, 4.0f * z.y * z.y};
+      }
+    }
+    wave_lds_sync();
+    // pair powers -> HTK mel -> ln(+1e-8), straight-line: lane l takes mel l
+    // over a fixed window of kMelW1 bins, and lanes 0-31 the halves of mel
+    // 64 + l / 2 over kMelW2 bins each (summed by a DPP swap); weights (x 1/4,
+    // zero outside the filter) and window starts are per-lane registers, so a
+    // tap is three 8-byte power reads (one per pair, immediate offsets) and
+    // three packed FMAs, with no per-lane trip count
+    {
+      const f2* p1 = PW + ws1;
+      const f2* p2 = PW + ws2;
+      f2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f}, a2 = {0.0f, 0.0f};
+      f2 c0 = {0.0f, 0.0f}, c1 = {0.0f, 0.0f}, c2 = {0.0f, 0.0f};
+#pragma unroll
+      for (int j = 0; j < kMelW1; ++j) {
+        a0 = fma2(p1[j], f2{mw1[j], mw1[j]}, a0);
+        a1 = fma2(p1[kP2Pitch + j], f2{mw1[j], mw1[j]}, a1);
+        a2 = fma2(p1[2 * kP2Pitch + j], f2{mw1[j], mw1[j]}, a2);
+      }
+#pragma unroll
+      for (int j = 0; j < kMelW2; ++j) {
+        c0 = fma2(p2[j], f2{mw2[j], mw2[j]}, c0);
+        c1 = fma2(p2[kP2Pitch + j], f2{mw2[j], mw2[j]}, c1);
+        c2 = fma2(p2[2 * kP2Pitch + j], f2{mw2[j], mw2[j]}, c2);
+      }
+      float cv[6] = {c0.x, c0.y, c1.x, c1.y, c2.x, c2.y};
+#pragma unroll
+      for (int f = 0; f < 6; ++f)   // + the other half (lane ^ 1)
+        cv[f] += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, cv[f]), 0xB1, 0xF, 0xF, false));
+      const int64_t r0 = ps * kRowsPerPass;
+      const float av[6] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y};
+      const bool half0 = lane < 2 * (kMels - 64) && (lane & 1) == 0;
+#pragma unroll
+      for (int f = 0; f < 6; ++f) {
+        if (r0 + f < rows) {
+          feats[(r0 + f) * kMels + lane] = wk_logf(av[f] + 1e-8f);
+          if (half0) feats[(r0 + f) * kMels + 64 + (lane >> 1)] = wk_logf(cv[f] + 1e-8f);
+        }
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
 // Global z-score of one utterance per block (ctc.py:101-104: mean, unbiased
 // std, applied only when std > 0).  Up to kZsCache float4 per thread stay in
 // registers between the two reductions and the write-back, so the utterance
@@ -766,32 +965,71 @@ __global__ __launch_bounds__(kGru16Threads, 4) void ctc_gru16_kernel(const __hal
 // A workgroup owns 32 utterances (two 16-row tiles) of one direction, one
 // workgroup per CU (8 waves, 2 per SIMD, up to 256 VGPRs each): wave w owns
 // units 16 w .. 16 w + 15 of the r, z and n gates for both row tiles, as in
-// ctc_gru16_kernel.  W_ih of those 48 rows is held as A fragments of
-// v_mfma_f32_16x16x32_f16 (k-steps of 32): k < 128 in VGPRs (48 registers),
-// k >= 128 (layer 1) in an LDS image in fragment order (96 KB per
-// workgroup).  Per step t a wave issues
-//   * the h-part of step t: 2 tiles x 3 gates x 8 MFMAs 16x16x16 on the fp16
-//     state image (accumulating onto the x-part of r and z; n keeps its h-part
-//     apart for r (.)),
-//   * the x-part of step t + 1 (independent of the state, so it fills the
-//     matrix pipe while the h-part chains drain and the gate math runs):
-//     2 tiles x 3 gates x DIN/32 MFMAs 16x16x32 on the staged x tile, the
-//     biases as their initial accumulator (b_ir + b_hr, b_iz + b_hz, b_in),
-// then the fp32 gate math and the new fp16 state, one barrier per step.  The x
-// rows of step t + 2 are staged through a double-buffered LDS tile from a
-// 2-step register ring of cooperative 16-byte loads (rows past B read 0 from
-// the buffer resource's range check); outputs leave as 16-byte pieces of the
-// state image, as in ctc_gru16_kernel.  The gate pre-activations stay in fp32
-// (the GEMM path rounds them to fp16).
+// ctc_gru16_kernel.  Its 48 rows of W_hh and W_ih are A fragments of
+// v_mfma_f32_16x16x32_f16 (k-steps of 32): W_hh and W_ih k < 128 in VGPRs
+// (2 x 48 registers), layer 1's W_ih k >= 128 in an LDS image in fragment
+// order (96 KB per workgroup).
+//
+// Gate pre-activations arrive pre-scaled for the exp2 unit: the r and z rows
+// of both weights and their biases carry -log2(e), the n rows (x-part and
+// h-part, b_in and b_hn) 2 log2(e), so r = 1 / (1 + 2^a), z likewise, and
+// tanh(v) = 1 - 2 / (2^v' + 1) take no scaling multiply.  Rows past B read 0
+// as x and their state is never stored (each utterance's recurrence is its
+// own), so the gate math runs on every lane unmasked.
+//
+// One step (one barrier), per wave:
+//   memory: the previous step's outputs (16-byte pieces of the state image),
+//     the x rows of step t + 2 into the LDS tile the previous step's x-part
+//     read (from a 2-step register ring of 16-byte loads), the ring refilled;
+//   h-part of step t, tile 0 (12 MFMAs onto the x-part accumulators of r and
+//     z; n's h-part apart, b_hn as its initial accumulator);
+//   h-part of tile 1 (12 MFMAs), interleaved with tile 0's gate math;
+//   x-part of step t + 1 (2 tiles x 3 gates x DIN/32 MFMAs on the staged x
+//     tile, biases as the initial accumulator), independent of the state,
+//     interleaved with tile 1's gate math;
+//   the new fp16 state into the other state image, barrier.
+// The interleave is fixed at compile time by sched_group_barrier, so the
+// matrix pipe and the gate VALU overlap inside each wave instead of taking
+// turns (phase stamps of the unscheduled form: the gate + x-part phase took
+// the sum of its MFMA and VALU times).
 // ---------------------------------------------------------------------------
 constexpr int kGxRows = 32;                       // utterances per workgroup
 constexpr int kGxWaves = 8, kGxThreads = 64 * kGxWaves;
 typedef _Float16 h8x __attribute__((ext_vector_type(8)));
+constexpr float kNegLog2e = -1.4426950408889634f, kTwoLog2e = 2.8853900817779268f;
+
+#ifndef WK_GRU_VPM0
+#define WK_GRU_VPM0 2   // VALU per MFMA beside tile 1's h-part
+#endif
+#ifndef WK_GRU_PRIO
+#define WK_GRU_PRIO 0   // experiment: issue priority 1 for the younger wave of each SIMD (waves 4-7)
+#endif
+#ifdef WK_GRU_STAMPS   // diagnostic build only (tools/debug/gru_stamps.py; needs -DWK_STAMPS): cycle sums per phase
+__device__ unsigned long long g_gru_stamps[2][kGxWaves][16];
+#define GRU_HIT(k)                                  \
+  do {                                              \
+    __builtin_amdgcn_sched_barrier(0);              \
+    _st.hit(k);                                     \
+    __builtin_amdgcn_sched_barrier(0);              \
+  } while (0)
+#else
+#define GRU_HIT(k) do {} while (0)
+#endif
+
+// One element of the GRU cell on pre-scaled pre-activations (see above):
+// ar = -log2e (r pre-activation), az likewise, gn = 2 log2e (W_in x + b_in),
+// an = 2 log2e (W_hn h + b_hn); returns h' = (1 - z) n + z h.
+__device__ __forceinline__ float gru_cell(float ar, float az, float gn, float an, float h) {
+  const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(ar));
+  const float z = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(az));
+  const float c = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(__builtin_fmaf(r, an, gn)) + 1.0f), 1.0f);
+  return __builtin_fmaf(z, h - c, c);
+}
 
 template <int DIN>
 __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half* __restrict__ x,
                                                                   const h8x* __restrict__ wih_pk,
-                                                                  const h4* __restrict__ whh_pk,
+                                                                  const h8x* __restrict__ whh_pk,
                                                                   const float* __restrict__ bih,
                                                                   const float* __restrict__ bhh, int64_t B, int T,
                                                                   __half* __restrict__ out) {
@@ -801,6 +1039,8 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
   constexpr int XP = DIN + 8;                  // x tile pitch (halves): 16-byte rows, conflict-free B reads
   constexpr int XCH = kGxRows * DIN / 8;       // 16-byte chunks per x tile
   constexpr int XPT = (XCH + kGxThreads - 1) / kGxThreads;   // per thread
+  // VALU per MFMA beside the x-part: the rest of the ~2 x 54 gate instructions
+  constexpr int VPM1 = (108 - 12 * WK_GRU_VPM0 + 6 * KX - 1) / (6 * KX) > 0 ? (108 - 12 * WK_GRU_VPM0 + 6 * KX - 1) / (6 * KX) : 1;
   __shared__ __attribute__((aligned(16))) _Float16 h16[2][kGxRows * kH16P];
   __shared__ __attribute__((aligned(16))) _Float16 xt[2][kGxRows * XP];
   __shared__ __attribute__((aligned(16))) h8x wl[KXL > 0 ? 3 * kGxWaves * KXL * 64 : 1];
@@ -812,19 +1052,18 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
   const int u0 = 16 * wave + 4 * lg;
   const int64_t b0 = (int64_t)blockIdx.x * kGxRows;
   const int nrow = (int)(B - b0 < kGxRows ? B - b0 : kGxRows);
-  const bool live0 = n < nrow, live1 = 16 + n < nrow;
-  // weights: W_hh (16x16x16 A fragments) and W_ih k < 128 (16x16x32) in VGPRs
-  h4 wr[8], wz[8], wn[8];
+  // weights (pre-scaled on the host): W_hh and W_ih k < 128 in VGPRs, [dir][gate][wave][ks][lane]
+  h8x wr[4], wz[4], wn[4];
   h8x xr[KXR], xz[KXR], xn[KXR];
   {
-    const h4* p = whh_pk + (size_t)dir * 24 * 8 * 64 + lane;
+    const h8x* p = whh_pk + (size_t)dir * 3 * kGxWaves * 4 * 64 + lane;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      wr[s] = p[((0 * 8 + wave) * 8 + s) * 64];
-      wz[s] = p[((1 * 8 + wave) * 8 + s) * 64];
-      wn[s] = p[((2 * 8 + wave) * 8 + s) * 64];
+    for (int s = 0; s < 4; ++s) {
+      wr[s] = p[((0 * kGxWaves + wave) * 4 + s) * 64];
+      wz[s] = p[((1 * kGxWaves + wave) * 4 + s) * 64];
+      wn[s] = p[((2 * kGxWaves + wave) * 4 + s) * 64];
     }
-    const h8x* q = wih_pk + (size_t)dir * 3 * kGxWaves * KX * 64 + lane;   // [dir][gate][wave][ks][lane]
+    const h8x* q = wih_pk + (size_t)dir * 3 * kGxWaves * KX * 64 + lane;
 #pragma unroll
     for (int s = 0; s < KXR; ++s) {
       xr[s] = q[((0 * kGxWaves + wave) * KX + s) * 64];
@@ -839,14 +1078,14 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
     }
   }
   for (int i = tid; i < kGxRows * kH16P; i += kGxThreads) h16[0][i] = (_Float16)0.0f;
-  if (tid < kH) {
+  if (tid < kH) {   // scaled biases: -log2e (b_ir + b_hr), -log2e (b_iz + b_hz), 2 log2e b_in, 2 log2e b_hn
     const float* bi = bih + dir * 3 * kH;
     const float* bh = bhh + dir * 3 * kH;
     float* gbf = reinterpret_cast<float*>(&gbias[0][0]);
-    gbf[tid] = bi[tid] + bh[tid];
-    gbf[kH + tid] = bi[kH + tid] + bh[kH + tid];
-    gbf[2 * kH + tid] = bi[2 * kH + tid];
-    gbf[3 * kH + tid] = bh[2 * kH + tid];
+    gbf[tid] = kNegLog2e * (bi[tid] + bh[tid]);
+    gbf[kH + tid] = kNegLog2e * (bi[kH + tid] + bh[kH + tid]);
+    gbf[2 * kH + tid] = kTwoLog2e * bi[2 * kH + tid];
+    gbf[3 * kH + tid] = kTwoLog2e * bh[2 * kH + tid];
   }
   // x rows of a step: 32 adjacent time-major rows, XCH 16-byte chunks, a
   // register ring kXPf steps deep, then the LDS tile of that step's parity
@@ -862,18 +1101,20 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
       xv[slot][c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, ch < XCH ? 16 * ch : 0x40000000, 0, 0));
     }
   };
+  static_assert(XCH % kGxThreads == 0, "x tile chunks divide over the threads (no guarded LDS write)");
   auto stage_x = [&](int slot, int buf) {
 #pragma unroll
     for (int c = 0; c < XPT; ++c) {
       const int ch = tid + c * kGxThreads;
-      if (ch < XCH) *reinterpret_cast<uint4*>(&xt[buf][(ch / (DIN / 8)) * XP + (ch % (DIN / 8)) * 8]) = xv[slot][c];
+      *reinterpret_cast<uint4*>(&xt[buf][(ch / (DIN / 8)) * XP + (ch % (DIN / 8)) * 8]) = xv[slot][c];
     }
   };
+  __syncthreads();   // gbias
+  int bq = u0 >> 2;
+  asm volatile("" : "+v"(bq));
+  const f32x4 b_r = gbias[0][bq], b_z = gbias[1][bq], b_n = gbias[2][bq], b_hn = gbias[3][bq];
   // x-part of one step from the x tile `buf` into g[tile][gate] (bias as the initial accumulator)
   auto xpart = [&](int buf, f32x4 (&g)[2][3]) {
-    int bq = u0 >> 2;
-    asm volatile("" : "+v"(bq));
-    const f32x4 b_r = gbias[0][bq], b_z = gbias[1][bq], b_n = gbias[2][bq];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       g[q][0] = b_r;
@@ -902,13 +1143,18 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
       }
     }
   };
-  const int64_t dstep = dir == 0 ? B : -B;   // out is time-major (row t B + b)
+  // Outputs (time-major rows t B + b, [fwd | bwd] halves): thread (row yn,
+  // chunk yc) stores 16 bytes of the state image per step through a buffer
+  // resource over the step's 32 rows, so rows past B fall outside num_records
+  // and are dropped -- no branch in the loop, and the compiler's vmcnt for the
+  // x-ring stays exact (a guarded store had made it wait for every store).
   const int yn = tid >> 4, yc = tid & 15;     // 512 threads = 32 rows x 16 chunks of the state image
-  const bool ylive = yn < nrow;
-  __half* yq = out + ((int64_t)(dir == 0 ? 0 : T - 1) * B + b0 + (ylive ? yn : 0)) * (2 * kH) + dir * kH + 8 * yc;
-  auto store_y = [&](int buf) {
-    if (ylive) *reinterpret_cast<uint4*>(yq) = *reinterpret_cast<const uint4*>(&h16[buf][yn * kH16P + 8 * yc]);
-    yq += dstep * (2 * kH);
+  const int yoff = yn * (2 * kH * 2) + dir * (kH * 2) + 16 * yc;
+  auto store_y = [&](int buf, int step_done, bool any) {   // the state after step step_done
+    const int t = dir == 0 ? step_done : T - 1 - step_done;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(out + ((int64_t)t * B + b0) * (2 * kH), any ? (uint32_t)nrow * (2 * kH * 2) : 0u);
+    const uint4 v = *reinterpret_cast<const uint4*>(&h16[buf][yn * kH16P + 8 * yc]);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), rs, yoff, 0, 0);
   };
   // prologue: x_0 and x_1 staged, x_2 / x_3 in the ring, gx of step 0
   load_x(0, 0);
@@ -923,57 +1169,82 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
   __syncthreads();   // x_0's tile is rewritten (with x_2) during step 0
   float h[2][4] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
   int cur = 0;
+#if WK_GRU_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+#ifdef WK_GRU_STAMPS
+  wk::WkStamps _st;
+  _st.init();
+#endif
   auto step_body = [&](int step, f32x4 (&g)[2][3], f32x4 (&gn)[2][3], int slot) {
-    // h-part of this step onto the x-part
-    f32x4 anh[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const _Float16* hb = h16[cur] + (16 * q + n) * kH16P + 4 * lg;
-      h4 hv[8];
-#pragma unroll
-      for (int s = 0; s < 8; ++s) hv[s] = *reinterpret_cast<const h4*>(hb + 16 * s);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        g[q][0] = __builtin_amdgcn_mfma_f32_16x16x16f16(wr[s], hv[s], g[q][0], 0, 0, 0);
-        g[q][1] = __builtin_amdgcn_mfma_f32_16x16x16f16(wz[s], hv[s], g[q][1], 0, 0, 0);
-        anh[q] = __builtin_amdgcn_mfma_f32_16x16x16f16(wn[s], hv[s], anh[q], 0, 0, 0);
-      }
-    }
-    // x-part of the next step (tile staged during the previous step)
-    if (step + 1 < T) xpart((step + 1) & 1, gn);
-    if (step > 0) store_y(cur);   // the previous step's outputs
-    // x rows of step + 2 into the tile this step's x-part was read from, then refill the ring slot
+    // memory work of the step (independent of the MFMAs): x rows of step + 2
+    // into the tile the previous step's x-part read, the previous step's
+    // outputs (none at step 0), the ring slot refilled
     stage_x(slot, step & 1);
+    store_y(cur, step - 1, step > 0);
     load_x(slot, step + 2 + kXPf);
-    int bq = u0 >> 2;
-    asm volatile("" : "+v"(bq));
-    const f32x4 bh_c = gbias[3][bq];
+    h8x hv[2][4];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const bool live = q == 0 ? live0 : live1;
-      h4 o;
+      const _Float16* hb = h16[cur] + (16 * q + n) * kH16P + 8 * lg;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) hv[q][s] = *reinterpret_cast<const h8x*>(hb + 32 * s);
+    }
+    GRU_HIT(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // h-part of this step onto the x-part (n's h-part apart, b_hn as its initial accumulator)
+    f32x4 anh[2] = {b_hn, b_hn};
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        g[q][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[s], hv[q][s], g[q][0], 0, 0, 0);
+        g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wz[s], hv[q][s], g[q][1], 0, 0, 0);
+        anh[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wn[s], hv[q][s], anh[q], 0, 0, 0);
+      }
+    // gate math of both tiles (tile 0 beside tile 1's h-part, tile 1 beside
+    // the x-part of the next step; the last step's x-part reads a stale tile
+    // and is discarded)
+    h4 o[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float hn = 0.0f;
-        if (live) {
-          const float r = sigm(g[q][0][i]);
-          const float z = sigm(g[q][1][i]);
-          const float c = tanh_fast(g[q][2][i] + r * (anh[q][i] + bh_c[i]));
-          hn = __builtin_fmaf(z, h[q][i] - c, c);   // (1 - z) c + z h
-        }
+        const float hn = gru_cell(g[q][0][i], g[q][1][i], g[q][2][i], anh[q][i], h[q][i]);
         h[q][i] = hn;
-        o[i] = (_Float16)hn;
+        o[q][i] = (_Float16)hn;
       }
-      *reinterpret_cast<uint2*>(&h16[cur ^ 1][(16 * q + n) * kH16P + u0]) = __builtin_bit_cast(uint2, o);
+    xpart((step + 1) & 1, gn);
+    __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);   // tile 0's h-part
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {                        // tile 1's h-part || tile 0's gates
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, WK_GRU_VPM0, 0);
     }
+#pragma unroll
+    for (int i = 0; i < 6 * KX; ++i) {                    // x-part || tile 1's gates
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, VPM1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    GRU_HIT(1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      *reinterpret_cast<uint2*>(&h16[cur ^ 1][(16 * q + n) * kH16P + u0]) = __builtin_bit_cast(uint2, o[q]);
     cur ^= 1;
+    GRU_HIT(2);
     __syncthreads();
+    GRU_HIT(3);
   };
   for (int step = 0; step < T; step += 2) {
     step_body(step, ga, gb, 0);
     if (step + 1 < T) step_body(step + 1, gb, ga, 1);
   }
-  store_y(cur);   // the last step's outputs
+  store_y(cur, T - 1, true);   // the last step's outputs
+#ifdef WK_GRU_STAMPS
+  if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int k = 0; k < 16; ++k) atomicAdd(&g_gru_stamps[DIN == 128 ? 0 : 1][wave][k], _st.st[k]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1431,7 +1702,8 @@ struct wk_ctc {
   float* zero_b;        // [V] zeros: the log_softmax kernel's bias in fp16 mode (the logits carry theirs)
   __half* wih16[2];     // fp16 copies (precision 1)
   __half* whh16_pk[2];  // per layer: [2 dir][24 tiles][8 k-steps][64 lanes][4]
-  __half* wih16x_pk[2]; // per layer: [2 dir][3 gates][8 waves][din/32 k-steps][64 lanes][8] (fused-projection GRU)
+  __half* whh16x_pk[2]; // per layer: [2 dir][3 gates][8 waves][4 k-steps][64 lanes][8] (W_hh as 16x16x32 fragments, gate-scaled)
+  __half* wih16x_pk[2]; // per layer: [2 dir][3 gates][8 waves][din/32 k-steps][64 lanes][8] (fused-projection GRU, gate-scaled)
   bool gru_gemm;        // fp16 mode: input projections as a separate GEMM (WAKEWORD_CTC_GEMM=1; A/B and checks)
   __half* out_w16;
   float* fft_win;       // [400] periodic Hann
@@ -1439,6 +1711,8 @@ struct wk_ctc {
   int *fb_start, *fb_len, *fb_off;
   float* fb_w;
   int n_fbw;            // CSR weight count (<= kFbMaxW)
+  float* melw;          // ctc_logmel_fft2_kernel: per-lane padded mel weights x 1/4, [64][kMelW1] then [64][kMelW2]
+  int* melws;           // their window start bins, [64] then [64]
   // workspaces (grown on demand)
   size_t ws_rows;
   float *x0, *gi, *y0, *y1, *logits;
@@ -1518,7 +1792,7 @@ void free_all(wk_ctc* c) {
   void* ps[] = {c->enc_w, c->enc_b, c->ln_g, c->ln_b, c->wih[0], c->wih[1], c->bih[0], c->bih[1], c->bhh[0],
                 c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->zero_b, c->fb_w, c->wih16[0], c->wih16[1],
                 c->out_w16, c->fft_win, c->fft_tw, c->fb_start, c->fb_len, c->fb_off, c->whh16_pk[0], c->whh16_pk[1],
-                c->wih16x_pk[0], c->wih16x_pk[1]};
+                c->wih16x_pk[0], c->wih16x_pk[1], c->whh16x_pk[0], c->whh16x_pk[1], c->melw, c->melws};
   for (void* q : ps) (void)hipFree(q);
   if (c->blas) rocblas_destroy_handle(c->blas);
 }
@@ -1589,10 +1863,11 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     if (e == hipSuccess) e = upload(&c->ln_b, ln_b, H);
     for (int l = 0; l < 2 && e == hipSuccess; ++l) {
       const int din = l == 0 ? H : 2 * H;
-      std::vector<float> wih(6 * (size_t)H * din), bih(6 * H), bhh(6 * H), pk(2 * 24 * 32 * 64), pk16(2 * 24 * 8 * 64 * 4);
+      std::vector<float> wih(6 * (size_t)H * din), whh_all(6 * (size_t)H * H), bih(6 * H), bhh(6 * H), pk(2 * 24 * 32 * 64), pk16(2 * 24 * 8 * 64 * 4);
       for (int d = 0; d < 2; ++d) {
         const float* wi = take(3 * (size_t)H * din);
         const float* wh = take(3 * (size_t)H * H);
+        memcpy(&whh_all[(size_t)d * 3 * H * H], wh, sizeof(float) * 3 * H * H);
         const float* bi = take(3 * H);
         const float* bh = take(3 * H);
         memcpy(&wih[(size_t)d * 3 * H * din], wi, sizeof(float) * 3 * H * din);
@@ -1612,6 +1887,8 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
       e = upload(&c->wih[l], wih.data(), wih.size());
       if (e == hipSuccess && c->f16) e = upload_f16(&c->wih16[l], wih.data(), wih.size());
       if (e == hipSuccess && c->f16) {   // W_ih as 16x16x32 A fragments: [dir][gate][wave][ks][lane][8]
+        // scaled for the fused kernel's exp2 gates: r, z rows by -log2(e), n rows by 2 log2(e)
+        const double gsc[3] = {-1.4426950408889634, -1.4426950408889634, 2.8853900817779268};
         const int kx = din / 32;
         std::vector<float> px((size_t)2 * 3 * 8 * kx * 64 * 8);
         size_t o = 0;
@@ -1621,8 +1898,18 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
               for (int ks = 0; ks < kx; ++ks)
                 for (int ln = 0; ln < 64; ++ln)
                   for (int j = 0; j < 8; ++j)
-                    px[o++] = wih[((size_t)d * 3 * H + g * H + 16 * w + (ln & 15)) * din + 32 * ks + 8 * (ln >> 4) + j];
+                    px[o++] = gsc[g] * wih[((size_t)d * 3 * H + g * H + 16 * w + (ln & 15)) * din + 32 * ks + 8 * (ln >> 4) + j];
         e = upload_f16(&c->wih16x_pk[l], px.data(), px.size());
+        std::vector<float> ph((size_t)2 * 3 * 8 * 4 * 64 * 8);   // W_hh the same way (k = H): [dir][gate][wave][ks][lane][8]
+        o = 0;
+        for (int d = 0; d < 2; ++d)
+          for (int g = 0; g < 3; ++g)
+            for (int w = 0; w < 8; ++w)
+              for (int ks = 0; ks < 4; ++ks)
+                for (int ln = 0; ln < 64; ++ln)
+                  for (int j = 0; j < 8; ++j)
+                    ph[o++] = gsc[g] * whh_all[((size_t)d * 3 * H + g * H + 16 * w + (ln & 15)) * H + 32 * ks + 8 * (ln >> 4) + j];
+        if (e == hipSuccess) e = upload_f16(&c->whh16x_pk[l], ph.data(), ph.size());
       }
       if (e == hipSuccess) e = upload(&c->bih[l], bih.data(), bih.size());
       if (e == hipSuccess) e = upload(&c->bhh[l], bhh.data(), bhh.size());
@@ -1671,6 +1958,34 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     if (e == hipSuccess) e = upload(&c->fb_w, wv.data(), wv.size());
     c->n_fbw = (int)wv.size();
     if (e == hipSuccess && c->n_fbw > kFbMaxW) e = hipErrorInvalidValue;   // LDS copy in ctc_logmel_fft_kernel
+    {   // straight-line windows of ctc_logmel_fft2_kernel (see there)
+      std::vector<float> mw((size_t)64 * (kMelW1 + kMelW2), 0.0f);
+      std::vector<int> ws(128, 0);
+      auto window = [&](int m, int wdt, int first, int lanes_w, float* dst, int* wsd) {
+        // window of wdt bins inside [0, kBins) covering the filter from bin `first`
+        int w0 = st[m] + first;
+        if (w0 + wdt > kBins) w0 = kBins - wdt;
+        *wsd = w0;
+        for (int j = 0; j < lanes_w; ++j) {
+          const int k = w0 + j;
+          const bool mine = k >= st[m] + first && k < st[m] + first + wdt && k <= st[m] + ln[m] - 1;
+          dst[j] = mine ? 0.25f * fb[(size_t)k * kMels + m] : 0.0f;
+        }
+      };
+      bool fits = kMels == 80;
+      for (int m = 0; m < 64 && fits; ++m) {
+        fits = ln[m] <= kMelW1;
+        window(m, kMelW1, 0, kMelW1, &mw[(size_t)m * kMelW1], &ws[m]);
+      }
+      for (int l = 0; l < 32 && fits; ++l) {
+        const int m = 64 + l / 2;
+        fits = ln[m] <= 2 * kMelW2;
+        window(m, kMelW2, (l & 1) * kMelW2, kMelW2, &mw[(size_t)64 * kMelW1 + (size_t)l * kMelW2], &ws[64 + l]);
+      }
+      if (e == hipSuccess && !fits) e = hipErrorInvalidValue;
+      if (e == hipSuccess) e = upload(&c->melw, mw.data(), mw.size());
+      if (e == hipSuccess) e = upload(&c->melws, ws.data(), ws.size());
+    }
     if (e != hipSuccess) {
       free_all(c);
       free(c);
@@ -1710,9 +2025,17 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
     // read a device table instead of a possibly empty audio buffer
     const float* au = nv > 0 ? d_audio : c->fft_win;
     wk_status s = timed(c, WK_CTC_STAGE_LOGMEL, st, [&]() -> wk_status {
+#ifdef WK_LOGMEL_V1
       hipLaunchKernelGGL(ctc_logmel_fft_kernel, dim3((unsigned)(blocks < 8 * c->n_cu ? blocks : 8 * c->n_cu)), dim3(256),
                          0, st, au, nv > 0 ? stride : (int64_t)0, nv, n_samples, T, rows, c->fft_win, c->fft_tw,
                          c->fb_start, c->fb_len, c->fb_off, c->fb_w, c->n_fbw, d_feats);
+#else
+      const int64_t passes2 = (rows + 2 * kF2Pairs - 1) / (2 * kF2Pairs);
+      const int64_t blocks2 = (passes2 + kF2Waves - 1) / kF2Waves;
+      hipLaunchKernelGGL(ctc_logmel_fft2_kernel, dim3((unsigned)(blocks2 < c->n_cu ? blocks2 : c->n_cu)), dim3(kF2Waves * 64),
+                         0, st, au, nv > 0 ? stride : (int64_t)0, nv, n_samples, T, rows, c->fft_win, c->fft_tw,
+                         c->melw, c->melws, d_feats);
+#endif
       return WK_OK;
     });
     if (s == WK_OK)
@@ -1781,10 +2104,10 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
         s = timed(c, WK_CTC_STAGE_GRU0 + 2 * l, st, [&]() -> wk_status {
           if (l == 0)
             hipLaunchKernelGGL(ctc_gru16x_kernel<128>, gx, dim3(kGxThreads), 0, st, in16, (const h8x*)c->wih16x_pk[0],
-                               (const h4*)c->whh16_pk[0], c->bih[0], c->bhh[0], batch, T, ys16[0]);
+                               (const h8x*)c->whh16x_pk[0], c->bih[0], c->bhh[0], batch, T, ys16[0]);
           else
             hipLaunchKernelGGL(ctc_gru16x_kernel<256>, gx, dim3(kGxThreads), 0, st, in16, (const h8x*)c->wih16x_pk[1],
-                               (const h4*)c->whh16_pk[1], c->bih[1], c->bhh[1], batch, T, ys16[1]);
+                               (const h8x*)c->whh16x_pk[1], c->bih[1], c->bhh[1], batch, T, ys16[1]);
           return WK_OK;
         });
         if (s != WK_OK) return s;
@@ -1900,3 +2223,14 @@ wk_status wk_ctc_frame_argmax(wk_ctc* c, int64_t batch, int32_t T, int32_t* d_pr
 }
 
 }  // extern "C"
+
+#ifdef WK_GRU_STAMPS
+extern "C" int wk_debug_gru_stamps(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_gru_stamps), sizeof(g_gru_stamps)) != hipSuccess) return 1;
+  if (reset) {
+    static unsigned long long zero[2][kGxWaves][16];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_gru_stamps), zero, sizeof(zero)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
