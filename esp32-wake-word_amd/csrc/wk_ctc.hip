@@ -1478,6 +1478,17 @@ constexpr int out_rf(bool logits) { return logits ? 2 : kOutRF; }
 constexpr int out_rows(bool logits) { return 16 * out_rf(logits) * kOutWaves; }
 static_assert(kOutPre * 64 * kOutWaves == kOutBN * (kOutK / 8), "W tile chunks divide over the threads");
 
+#ifdef WK_OUT_STAMPS   // diagnostic build only (tools/debug/out_stamps.py; needs -DWK_STAMPS): cycle sums per phase
+__device__ unsigned long long g_out_stamps[kOutWaves][16];
+#define OUT_HIT(k)                                  \
+  do {                                              \
+    __builtin_amdgcn_sched_barrier(0);              \
+    _st.hit(k);                                     \
+    __builtin_amdgcn_sched_barrier(0);              \
+  } while (0)
+#else
+#define OUT_HIT(k) do {} while (0)
+#endif
 template <bool LOGITS>
 __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const __half* __restrict__ y,
                                                                           const __half* __restrict__ w,
@@ -1604,10 +1615,15 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #if WK_OUT_PRIO
   if (lag) __builtin_amdgcn_s_setprio(1);
 #endif
+#ifdef WK_OUT_STAMPS
+  wk::WkStamps _st;
+  _st.init();
+#endif
   for (int nt = 0; nt < NT; ++nt) {
     if (nt + 1 < NT) fetch(nt + 1);
     const _Float16* b = bt[nt & 1];
     if (lag && nt > 0) epilogue(nt - 1);
+    OUT_HIT(0);
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       h8 bf[4];
@@ -1630,20 +1646,29 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
             acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf[cf], acc[rf][cf], 0, 0, 0);
       }
     }
+    OUT_HIT(1);
 #if WK_OUT_DMA
     if (!lag && nt + 1 < NT) {   // after this wave's last LDS read of the period
       stash((nt + 1) & 1);
       dma_w(nt + 1);
     }
 #endif
+    OUT_HIT(2);
     if (!lag) epilogue(nt);
+    OUT_HIT(3);
 #if WK_OUT_DMA
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // LDS-DMA done (the barrier's own wait omits it)
 #else
     if (nt + 1 < NT) stash((nt + 1) & 1);
 #endif
+    OUT_HIT(4);
     __syncthreads();
+    OUT_HIT(5);
   }
+#ifdef WK_OUT_STAMPS
+  if (lane == 0 && blockIdx.x == 0 && !LOGITS)
+    for (int k = 0; k < 16; ++k) atomicAdd(&g_out_stamps[wv][k], _st.st[k]);
+#endif
   if (lag && NT > 0) epilogue(NT - 1);
   // first maximum across the 16 column lanes of each row
 #pragma unroll
@@ -2230,6 +2255,17 @@ extern "C" int wk_debug_gru_stamps(unsigned long long* host_out, int reset) {
   if (reset) {
     static unsigned long long zero[2][kGxWaves][16];
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_gru_stamps), zero, sizeof(zero)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
+
+#ifdef WK_OUT_STAMPS
+extern "C" int wk_debug_out_stamps(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_out_stamps), sizeof(g_out_stamps)) != hipSuccess) return 1;
+  if (reset) {
+    static unsigned long long zero[kOutWaves][16];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_out_stamps), zero, sizeof(zero)) != hipSuccess) return 1;
   }
   return 0;
 }
