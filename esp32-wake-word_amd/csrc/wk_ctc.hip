@@ -278,7 +278,11 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
 constexpr int kF2Waves = 12, kF2Pairs = 3;
 constexpr int kMelW1 = 8, kMelW2 = 7;   // mel windows: mels 0-63 <= 8 bins, mels 64-79 <= 14 = 2 x 7 (host-checked)
 constexpr int kA2Pitch = 25;    // A[g][n2][k1] rows (float2): 25 = 1 mod 8 -> stage-2 lane groups start 40 banks apart
-constexpr int kE2Pitch = 12;    // exchange rows (float2), 16-byte aligned for the b128 writes
+#ifndef WK_E2_PITCH
+#define WK_E2_PITCH 11
+#endif
+constexpr int kE2Pitch = WK_E2_PITCH;   // exchange rows (float2): 22 dwords -> 20 partner rows on distinct banks
+                                // (pitch 12 put them on 8 bank pairs: 24 p mod 64 has period 8)
 constexpr int kP2Pitch = 212;   // pair-power rows (float2): 2 x 212 = 40 mod 64 banks between lane groups
 static_assert(kF2Pairs * kP2Pitch <= kF2Pairs * 20 * kA2Pitch, "power rows alias the A region");
 static_assert(kF2Pairs * 20 * kE2Pitch <= kF2Pairs * 20 * kA2Pitch, "exchange rows alias the A region");
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     if (lact) {
       f2* e = E + (g * 20 + q) * kE2Pitch;
 #pragma unroll
-      for (int j = 0; j < 10; j += 2) *reinterpret_cast<f32x4*>(e + j) = f32x4{v[10 + j].x, v[10 + j].y, v[11 + j].x, v[11 + j].y};
+      for (int j = 0; j < 10; ++j) e[j] = v[10 + j];
       if (q == 0) e[10] = v[0];
     }
     wave_lds_sync();
