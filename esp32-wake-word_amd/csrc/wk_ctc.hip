@@ -304,7 +304,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
   for (int i = threadIdx.x; i < kNfft; i += NT) L.win[i] = win_g[i];
   for (int i = threadIdx.x; i < 400; i += NT) L.tw[i / 20][i % 20] = f2{tw_g[2 * i], tw_g[2 * i + 1]};
   __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (buffer resources)
   const int g = lane / 20, q = lane - 20 * (lane / 20);   // pair slot (3 = idle lanes 60-63), n2 / k1
   f2* A = L.w[wv];
   constexpr int kRowsPerPass = 2 * kF2Pairs;
@@ -314,12 +314,8 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
   // The lane's 20 samples x[20 n1 + q] of one frame (row) of pass ps_; idle
   // lanes and rows past the end read utterance 0's first samples (nothing
   // they compute is stored).  Wave-uniform paths, exactly 20 loads each.
-  auto load_raw = [&](int64_t ps_, int fo, float (&raw)[20]) {
-    const int64_t row = ps_ * kRowsPerPass + 2 * g + fo;
-    const bool live = g < kF2Pairs && ps_ < passes && row < rows;
-    const int rr = live ? (int)row : 0;   // rows < 2^31 (host check)
-    const int b = (int)((unsigned)rr / (unsigned)T), t = rr - b * T;
-    const float* xa = audio + (int64_t)b * stride;
+  auto load_one = [&](bool live, int b, int t, float (&raw)[20]) {
+    const float* xa = audio + (int64_t)(live ? b : 0) * stride;
     const int p0 = live ? t * kHop - kNfft / 2 : 0;
     if (__all(p0 >= 0 && p0 + kNfft <= nv_min)) {
       const float* xp = xa + p0 + q;
@@ -337,6 +333,18 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
       }
     }
   };
+  // both frames of the lane group's pair: one division for frame a, frame b is
+  // the next row (t + 1, or frame 0 of the next utterance)
+  auto load_pair = [&](int64_t ps_, float (&ra_)[20], float (&rb_)[20]) {
+    const int64_t row = ps_ * kRowsPerPass + 2 * g;
+    const bool live_a = g < kF2Pairs && ps_ < passes && row < rows;
+    const bool live_b = live_a && row + 1 < rows;
+    const int rr = live_a ? (int)row : 0;   // rows < 2^31 (host check)
+    const int ba = (int)((unsigned)rr / (unsigned)T), ta = rr - ba * T;
+    const bool wrap = ta + 1 == T;
+    load_one(live_a, ba, ta, ra_);
+    load_one(live_b, wrap ? ba + 1 : ba, wrap ? 0 : ta + 1, rb_);
+  };
   // the lane's mel windows: mel `lane` (kMelW1 taps from bin ws1) and half
   // `lane & 1` of mel 64 + lane / 2 (kMelW2 taps from ws2; lanes >= 32: zero weights)
   float mw1[kMelW1], mw2[kMelW2];
@@ -346,8 +354,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
   for (int j = 0; j < kMelW2; ++j) mw2[j] = melw[64 * kMelW1 + lane * kMelW2 + j];
   const int ws1 = melws[lane], ws2 = melws[64 + lane];
   float ra[20], rb[20];
-  load_raw((int64_t)blockIdx.x * kF2Waves + wv, 0, ra);
-  load_raw((int64_t)blockIdx.x * kF2Waves + wv, 1, rb);
+  load_pair((int64_t)blockIdx.x * kF2Waves + wv, ra, rb);
   const bool lact = g < kF2Pairs;
   for (int64_t ps = (int64_t)blockIdx.x * kF2Waves + wv; ps < passes; ps += pstep) {
     // stage 1: lane (g, n2 = q): DFT-20 over n1 of z[20 n1 + n2] = w (x_a + i x_b)
@@ -358,8 +365,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
       v[n1] = f2{ra[n1], rb[n1]} * f2{wn, wn};
       asm volatile("" ::"v"(v[n1].x), "v"(v[n1].y) : "memory");   // ahead of the next pass's loads
     }
-    load_raw(ps + pstep, 0, ra);
-    load_raw(ps + pstep, 1, rb);
+    load_pair(ps + pstep, ra, rb);
     dft20(v);
     // A rows: lane (g, q) writes A[g][q][0..19]; pitch 25 float2 = 50 dwords:
     // 50 i mod 64 over 32 lanes is 2 x (25 i mod 32), all distinct
@@ -438,15 +444,21 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
 #pragma unroll
       for (int f = 0; f < 6; ++f)   // + the other half (lane ^ 1)
         cv[f] += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, cv[f]), 0xB1, 0xF, 0xF, false));
+      // stores through a resource over the pass's rows: rows past the end
+      // fall outside num_records, and lanes 1, 3, ... of the second set (odd
+      // halves) and 32-63 aim past it too -- no branch per frame
       const int64_t r0 = ps * kRowsPerPass;
+      const int64_t nr = rows - r0 < kRowsPerPass ? rows - r0 : kRowsPerPass;
+      const __amdgpu_buffer_rsrc_t fr = make_rsrc(feats + r0 * kMels, (uint32_t)(nr > 0 ? nr : 0) * kMels * 4);
       const float av[6] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y};
       const bool half0 = lane < 2 * (kMels - 64) && (lane & 1) == 0;
+      const int o2 = half0 ? 4 * (64 + (lane >> 1)) : 0x40000000;
 #pragma unroll
       for (int f = 0; f < 6; ++f) {
-        if (r0 + f < rows) {
-          feats[(r0 + f) * kMels + lane] = wk_logf(av[f] + 1e-8f);
-          if (half0) feats[(r0 + f) * kMels + 64 + (lane >> 1)] = wk_logf(cv[f] + 1e-8f);
-        }
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, wk_logf(av[f] + 1e-8f)), fr,
+                                              4 * (f * kMels + lane), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, wk_logf(cv[f] + 1e-8f)), fr,
+                                              o2 + 4 * f * kMels, 0, 0);
       }
     }
     wave_lds_sync();
