@@ -662,21 +662,36 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
   __syncthreads();
   const int li = lane & 15, lg = lane >> 4;
   const int64_t nblk = (rows + 15) / 16;
-  for (int64_t blk = (int64_t)blockIdx.x * 4 + wv; blk < nblk; blk += (int64_t)gridDim.x * 4) {
+  // Loads and stores go through buffer resources (rows past the end read 0 /
+  // drop), so the loop has no branch: the next block's rows are loaded before
+  // this block's compute and stores, and the compiler's vmcnt waits for those
+  // loads only, not for the stores behind them (with guarded accesses it
+  // waited for everything: ~60 % of wave-cycles were waits, PMC).
+  const __amdgpu_buffer_rsrc_t irs = make_rsrc(in, (uint32_t)(rows * kMels * 4));   // < 2^31 B (host check)
+  const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, (uint32_t)(rows * kH * 2));
+  float4 xr[KS][2];
+  auto load_blk = [&](int64_t blk) {
+    const int64_t r = blk * 16 + li;
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int k0 = 32 * st + 8 * lg;
+      const int off = r < rows && k0 < kMels ? (int)(r * kMels + k0) * 4 : 0x7FFFFFE0;   // past num_records: 0
+      xr[st][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(irs, off, 0, 0));
+      xr[st][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(irs, off + 16, 0, 0));
+    }
+  };
+  int64_t blk = (int64_t)blockIdx.x * 4 + wv;
+  load_blk(blk);
+  for (; blk < nblk; blk += (int64_t)gridDim.x * 4) {
     const int64_t r = blk * 16 + li;   // this lane's row
     h8e xb[KS];
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
-      const int k0 = 32 * st + 8 * lg;
-      float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = a;
-      if (r < rows && k0 < kMels) {
-        const float4* p = reinterpret_cast<const float4*>(in + r * kMels + k0);
-        a = p[0];
-        b = p[1];
-      }
+      const float4 a = xr[st][0], b = xr[st][1];
       xb[st] = h8e{(_Float16)a.x, (_Float16)a.y, (_Float16)a.z, (_Float16)a.w,
                    (_Float16)b.x, (_Float16)b.y, (_Float16)b.z, (_Float16)b.w};
     }
+    load_blk(blk + (int64_t)gridDim.x * 4);   // the next block (past the end: zeros, unused)
     f32x4 acc[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc[ct] = *reinterpret_cast<const f32x4*>(&pb[0][16 * ct + 4 * lg]);   // + bias
@@ -705,19 +720,19 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
     s2 += __shfl_xor(s2, 16, 64);
     s2 += __shfl_xor(s2, 32, 64);
     const float rs = 1.0f / sqrtf(s2 * (1.0f / kH) + 1e-5f);   // biased variance, as nn.LayerNorm
-    if (r < rows) {
-      const int ub = (int)r / T, ut = (int)r - ub * T;   // rows < 2^31 (host check)
-      __half* orow = out + ((int64_t)ut * B + ub) * kH;
+    const int rr = r < rows ? (int)r : 0;   // rows < 2^31 (host check)
+    const int ub = rr / T, ut = rr - ub * T;
+    const int orow = r < rows ? (ut * B + ub) * (kH * 2) : 0x7FFFFE00;   // time-major output row (bytes); past the end: dropped
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        const int c0 = 16 * ct + 4 * lg;
-        const f32x4 g = *reinterpret_cast<const f32x4*>(&pb[1][c0]);
-        const f32x4 bt = *reinterpret_cast<const f32x4*>(&pb[2][c0]);
-        _Float16 y[4];
+    for (int ct = 0; ct < CT; ++ct) {
+      const int c0 = 16 * ct + 4 * lg;
+      const f32x4 g = *reinterpret_cast<const f32x4*>(&pb[1][c0]);
+      const f32x4 bt = *reinterpret_cast<const f32x4*>(&pb[2][c0]);
+      _Float16 y[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) y[i] = (_Float16)fmaxf(__builtin_fmaf((acc[ct][i] - mean) * rs, g[i], bt[i]), 0.0f);
-        *reinterpret_cast<uint2*>(orow + c0) = __builtin_bit_cast(uint2, y);
-      }
+      for (int i = 0; i < 4; ++i) y[i] = (_Float16)fmaxf(__builtin_fmaf((acc[ct][i] - mean) * rs, g[i], bt[i]), 0.0f);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, y), ors,
+                                            orow + c0 * 2, 0, 0);
     }
   }
 }
@@ -2099,6 +2114,8 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
   const int64_t rows = batch * (int64_t)T;
   if (rows > INT32_MAX) return invalid("wk_ctc_forward: batch x frames exceeds 2^31 rows");
   const bool f16 = c->f16;
+  // fp16 encoder: 32-bit buffer offsets over the [rows][80] fp32 features
+  if (f16 && rows * kMels * 4 >= (int64_t)0x7FFFFF00) return invalid("wk_ctc_forward: fp16 mode takes < 6.7 M rows per call");
   return on_device(c->cfg.device, [&]() -> wk_status {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
