@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include <math.h>
+#include <type_traits>
 #include <vector>
 
 #include <hip/hip_fp16.h>
@@ -1623,12 +1624,14 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   // The bias is the MFMAs' initial C operand (one ds_read_b128 of the
   // replicated bias per column tile), so the epilogue is compare + select.
   f32x4 acc[kOutRF][4];
-  auto epilogue = [&](int tile) {
+  // (FULL: every column of the tile is < V -- all tiles but a ragged last
+  // one -- so the per-lane bound check and its exec-mask blocks go)
+  auto epilogue_t = [&](int tile, auto full) {
     // column v = 64 tile + 16 cf + li, rows row0 + 16 rf + 4 lg + i
 #pragma unroll
     for (int cf = 0; cf < 4; ++cf) {
       const int v = tile * kOutBN + 16 * cf + li;
-      if (v < V) {
+      if (decltype(full)::value || v < V) {
 #pragma unroll
         for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
@@ -1642,6 +1645,10 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
           }
       }
     }
+  };
+  auto epilogue = [&](int tile) {
+    if ((tile + 1) * kOutBN <= V) epilogue_t(tile, std::true_type{});
+    else epilogue_t(tile, std::false_type{});
   };
 #if WK_OUT_PRIO
   if (lag) __builtin_amdgcn_s_setprio(1);
