@@ -1565,13 +1565,21 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   // vmcnt(0) before the closing barrier completes the DMA.
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
   constexpr int kDmaWaves = kOutWaves / 2, kDmaPer = kOutBN * kOutK * 2 / 1024 / kDmaWaves;
+  // per-lane global offsets within a tile are tile-invariant: computed once,
+  // the tile's base goes in the scalar offset
+  int dma_off[kDmaPer];
+#pragma unroll
+  for (int i = 0; i < kDmaPer; ++i) {
+    const int q = (wvu < kDmaWaves ? wvu : 0) * kDmaPer + i, rr = 2 * q + (lane >> 5), c = (lane & 31) ^ (rr & 15);
+    dma_off[i] = rr * (kOutK * 2) + 16 * c;
+  }
   auto dma_w = [&](int nt) {
     if (wvu >= kDmaWaves) return;
 #pragma unroll
     for (int i = 0; i < kDmaPer; ++i) {
-      const int q = wvu * kDmaPer + i, rr = 2 * q + (lane >> 5), c = (lane & 31) ^ (rr & 15);
+      const int q = wvu * kDmaPer + i;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)&bt[nt & 1][q * 512], 16,
-                                               (nt * kOutBN + rr) * (kOutK * 2) + 16 * c, 0, 0, 0);
+                                               dma_off[i], nt * (kOutBN * kOutK * 2), 0, 0);
     }
   };
   auto fetch = [&](int nt) {   // the tile's bias (W comes by dma_w)
