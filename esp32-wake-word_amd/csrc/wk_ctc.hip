@@ -1573,14 +1573,15 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     const int q = (wvu < kDmaWaves ? wvu : 0) * kDmaPer + i, rr = 2 * q + (lane >> 5), c = (lane & 31) ^ (rr & 15);
     dma_off[i] = rr * (kOutK * 2) + 16 * c;
   }
+  auto dma_piece = [&](int nt, int i) {
+    const int q = wvu * kDmaPer + i;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)&bt[nt & 1][q * 512], 16,
+                                             dma_off[i], nt * (kOutBN * kOutK * 2), 0, 0);
+  };
   auto dma_w = [&](int nt) {
     if (wvu >= kDmaWaves) return;
 #pragma unroll
-    for (int i = 0; i < kDmaPer; ++i) {
-      const int q = wvu * kDmaPer + i;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)&bt[nt & 1][q * 512], 16,
-                                               dma_off[i], nt * (kOutBN * kOutK * 2), 0, 0);
-    }
+    for (int i = 0; i < kDmaPer; ++i) dma_piece(nt, i);
   };
   auto fetch = [&](int nt) {   // the tile's bias (W comes by dma_w)
     if (wave0) pb = buf_load(brs, 4 * (nt * kOutBN + tid), 0);
@@ -1634,10 +1635,19 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   f32x4 acc[kOutRF][4];
   // (FULL: every column of the tile is < V -- all tiles but a ragged last
   // one -- so the per-lane bound check and its exec-mask blocks go)
-  auto epilogue_t = [&](int tile, auto full) {
+#ifndef WK_OUT_DMA_SPREAD
+#define WK_OUT_DMA_SPREAD 0   // (measured -2 to -4 %, not kept) the leading waves' LDS-DMA pieces issued between the epilogue's column blocks
+#endif
+  auto epilogue_t = [&](int tile, auto full, int dma_tile) {
     // column v = 64 tile + 16 cf + li, rows row0 + 16 rf + 4 lg + i
 #pragma unroll
     for (int cf = 0; cf < 4; ++cf) {
+#if WK_OUT_DMA
+      if (dma_tile >= 0) {
+#pragma unroll
+        for (int i = cf * kDmaPer / 4; i < (cf + 1) * kDmaPer / 4; ++i) dma_piece(dma_tile, i);
+      }
+#endif
       const int v = tile * kOutBN + 16 * cf + li;
       if (decltype(full)::value || v < V) {
 #pragma unroll
@@ -1654,9 +1664,9 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       }
     }
   };
-  auto epilogue = [&](int tile) {
-    if ((tile + 1) * kOutBN <= V) epilogue_t(tile, std::true_type{});
-    else epilogue_t(tile, std::false_type{});
+  auto epilogue = [&](int tile, int dma_tile = -1) {
+    if ((tile + 1) * kOutBN <= V) epilogue_t(tile, std::true_type{}, dma_tile);
+    else epilogue_t(tile, std::false_type{}, dma_tile);
   };
 #if WK_OUT_PRIO
   if (lag) __builtin_amdgcn_s_setprio(1);
@@ -1696,11 +1706,11 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #if WK_OUT_DMA
     if (!lag && nt + 1 < NT) {   // after this wave's last LDS read of the period
       stash((nt + 1) & 1);
-      dma_w(nt + 1);
+      if (!WK_OUT_DMA_SPREAD) dma_w(nt + 1);
     }
 #endif
     OUT_HIT(2);
-    if (!lag) epilogue(nt);
+    if (!lag) epilogue(nt, WK_OUT_DMA && WK_OUT_DMA_SPREAD && nt + 1 < NT && wvu < kDmaWaves ? nt + 1 : -1);
     OUT_HIT(3);
 #if WK_OUT_DMA
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // LDS-DMA done (the barrier's own wait omits it)
