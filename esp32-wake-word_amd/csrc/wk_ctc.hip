@@ -1521,7 +1521,7 @@ __device__ __forceinline__ int out_chunk(int n, int c) { return c ^ (n & 15); }
 constexpr int kOutPre = kOutBN * (kOutK / 8) / (64 * kOutWaves);
 constexpr int out_rf(bool logits) { return logits ? 2 : kOutRF; }
 constexpr int out_rows(bool logits) { return 16 * out_rf(logits) * kOutWaves; }
-static_assert(kOutPre * 64 * kOutWaves == kOutBN * (kOutK / 8), "W tile chunks divide over the threads");
+static_assert(WK_OUT_DMA || kOutPre * 64 * kOutWaves == kOutBN * (kOutK / 8), "W tile chunks divide over the threads");
 
 #ifdef WK_OUT_STAMPS   // diagnostic build only (tools/debug/out_stamps.py; needs -DWK_STAMPS): cycle sums per phase
 __device__ unsigned long long g_out_stamps[kOutWaves][16];
@@ -1577,7 +1577,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   // the target buffer was last read in the previous period, and the explicit
   // vmcnt(0) before the closing barrier completes the DMA.
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
-  constexpr int kDmaWaves = kOutWaves / 2, kDmaPer = kOutBN * kOutK * 2 / 1024 / kDmaWaves;
+  constexpr int kDmaWaves = 4, kDmaPer = kOutBN * kOutK * 2 / 1024 / kDmaWaves;   // waves 0-3 (leading) issue the DMA
   // per-lane global offsets within a tile are tile-invariant: computed once,
   // the tile's base goes in the scalar offset
   int dma_off[kDmaPer];
@@ -1642,7 +1642,9 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   // The barrier keeps all waves on one tile; the skew puts one wave's epilogue
   // VALU beside its partner's MFMAs instead of both SIMD waves alternating
   // all-MFMA and all-VALU phases in step.
-  const bool lag = WK_OUT_SKEW && __builtin_amdgcn_readfirstlane(wv) >= kOutWaves / 2;
+  // lagging: waves 4-7 (with 8 waves, one of the two waves of each SIMD; with
+  // 12, one of three)
+  const bool lag = WK_OUT_SKEW && ((__builtin_amdgcn_readfirstlane(wv) >> 2) & 1);
   // The bias is the MFMAs' initial C operand (one ds_read_b128 of the
   // replicated bias per column tile), so the epilogue is compare + select.
   f32x4 acc[kOutRF][4];
