@@ -466,6 +466,17 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
   }
 }
 
+// Sum over the four lanes l, l ^ 16, l ^ 32, l ^ 48 (a row's four 16-lane
+// groups), in every lane: gfx950's v_permlane16/32_swap exchange rows in the
+// VALU (with both operands the same register, the two results are the
+// lane's and its partner's values), no LDS round trip as __shfl_xor costs.
+__device__ __forceinline__ float sum_rows4(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
 // Global z-score of one utterance per block (ctc.py:101-104: mean, unbiased
 // std, applied only when std > 0).  Up to kZsCache float4 per thread stay in
 // registers between the two reductions and the write-back, so the utterance
@@ -707,8 +718,7 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
     float s1 = 0.0f;
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) s1 += (acc[ct][0] + acc[ct][1]) + (acc[ct][2] + acc[ct][3]);
-    s1 += __shfl_xor(s1, 16, 64);
-    s1 += __shfl_xor(s1, 32, 64);
+    s1 = sum_rows4(s1);
     const float mean = s1 * (1.0f / kH);
     float s2 = 0.0f;
 #pragma unroll
@@ -718,8 +728,7 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
         const float d = acc[ct][i] - mean;
         s2 = __builtin_fmaf(d, d, s2);
       }
-    s2 += __shfl_xor(s2, 16, 64);
-    s2 += __shfl_xor(s2, 32, 64);
+    s2 = sum_rows4(s2);
     const float rs = 1.0f / sqrtf(s2 * (1.0f / kH) + 1e-5f);   // biased variance, as nn.LayerNorm
     const int rr = r < rows ? (int)r : 0;   // rows < 2^31 (host check)
     const int ub = rr / T, ut = rr - ub * T;
