@@ -276,7 +276,10 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
 // LDS pitches (see the per-access notes) keep the stage-1 writes, stage-2
 // reads and pair-power writes free of bank conflicts.
 // ---------------------------------------------------------------------------
-constexpr int kF2Waves = 12, kF2Pairs = 3;
+#ifndef WK_LM_REGTW
+#define WK_LM_REGTW 0   // (measured 0.59 vs 0.48 ms: 2 waves per SIMD lose more than the LDS reads save) 1: window and twiddles of the lane in registers, 8 waves per workgroup (2 per SIMD)
+#endif
+constexpr int kF2Waves = WK_LM_REGTW ? 8 : 12, kF2Pairs = 3;
 constexpr int kMelW1 = 8, kMelW2 = 7;   // mel windows: mels 0-63 <= 8 bins, mels 64-79 <= 14 = 2 x 7 (host-checked)
 constexpr int kA2Pitch = 25;    // A[g][n2][k1] rows (float2): 25 = 1 mod 8 -> stage-2 lane groups start 40 banks apart
 #ifndef WK_E2_PITCH
@@ -307,6 +310,15 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (buffer resources)
   const int g = lane / 20, q = lane - 20 * (lane / 20);   // pair slot (3 = idle lanes 60-63), n2 / k1
+  float wreg[WK_LM_REGTW ? 20 : 1];
+  f2 twreg[WK_LM_REGTW ? 20 : 1];
+  if constexpr (WK_LM_REGTW) {
+#pragma unroll
+    for (int j = 0; j < 20; ++j) {
+      wreg[j] = L.win[20 * j + q];
+      twreg[j] = L.tw[q][j];
+    }
+  }
   f2* A = L.w[wv];
   constexpr int kRowsPerPass = 2 * kF2Pairs;
   const int64_t passes = (rows + kRowsPerPass - 1) / kRowsPerPass;
@@ -362,7 +374,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     f2 v[20];
 #pragma unroll
     for (int n1 = 0; n1 < 20; ++n1) {
-      const float wn = L.win[20 * n1 + q];
+      const float wn = WK_LM_REGTW ? wreg[n1] : L.win[20 * n1 + q];
       v[n1] = f2{ra[n1], rb[n1]} * f2{wn, wn};
       asm volatile("" ::"v"(v[n1].x), "v"(v[n1].y) : "memory");   // ahead of the next pass's loads
     }
@@ -379,7 +391,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     // 40 g x 25 = 40 g mod 64 dwords, so half-waves touch disjoint banks
     if (lact) {
 #pragma unroll
-      for (int n2 = 0; n2 < 20; ++n2) v[n2] = cmul2(A[(g * 20 + n2) * kA2Pitch + q], L.tw[q][n2]);
+      for (int n2 = 0; n2 < 20; ++n2) v[n2] = cmul2(A[(g * 20 + n2) * kA2Pitch + q], WK_LM_REGTW ? twreg[n2] : L.tw[q][n2]);
     }
     dft20(v);   // Z[q + 20 k2] in v[k2]
     // exchange (the A reads of this wave are done: one wave's LDS ops complete in order)

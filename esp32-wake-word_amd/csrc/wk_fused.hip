@@ -8,7 +8,7 @@
 // each clip's log-mel image [40][63] into one of two LDS buffers.  Waves 8-15
 // (CNN role) take the DCT-II + CMVN from that buffer into the conv1 input
 // image (one wave per clip, on the matrix cores: dct_cmvn_clip), then run the
-// CNN of wk_cnn.hip on batches of NBF = 4 clips.  The
+// CNN of wk_cnn_dev.h on batches of NBF = 4 clips.  The
 // roles share no s_barrier: each synchronises its own 8 waves through an LDS
 // counter barrier, and the hand-off is two LDS counters (log-mel ready /
 // log-mel buffer free).  Moving the DCT + CMVN to the CNN waves (which wait
