@@ -1065,6 +1065,9 @@ constexpr float kNegLog2e = -1.4426950408889634f, kTwoLog2e = 2.8853900817779268
 #ifndef WK_GRU_LDSABL
 #define WK_GRU_LDSABL 0   // diagnostic: LDS access sites replaced by register values (bitmask; wrong results)
 #endif
+#ifndef WK_GRU_FLAGS
+#define WK_GRU_FLAGS 0   // experiment: per-wave step counters instead of the step barrier (see the kernel)
+#endif
 #ifndef WK_GRU_PRIO
 #define WK_GRU_PRIO 0   // experiment: issue priority 1 for the younger wave of each SIMD (waves 4-7)
 #endif
@@ -1109,6 +1112,10 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
   __shared__ __attribute__((aligned(16))) _Float16 xt[2][kGxRows * XP];
   __shared__ __attribute__((aligned(16))) h8x wl[KXL > 0 ? 3 * kGxWaves * KXL * 64 : 1];
   __shared__ f32x4 gbias[4][kH / 4];
+  // WK_GRU_FLAGS: per-wave step counters replace the step barrier (flags[w] =
+  // steps wave w has finished, its state slice and x-tile writes complete);
+  // flags[8] is the abort word of the bounded spins
+  __shared__ __attribute__((aligned(16))) unsigned gflags[12];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int dir = blockIdx.y;
@@ -1142,6 +1149,7 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
     }
   }
   for (int i = tid; i < kGxRows * kGxHP; i += kGxThreads) h16[0][i] = (_Float16)0.0f;
+  if (tid < 12) gflags[tid] = 0u;
   if (tid < kH) {   // scaled biases: -log2e (b_ir + b_hr), -log2e (b_iz + b_hz), 2 log2e b_in, 2 log2e b_hn
     const float* bi = bih + dir * 3 * kH;
     const float* bh = bhh + dir * 3 * kH;
@@ -1242,7 +1250,65 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
   wk::WkStamps _st;
   _st.init();
 #endif
+#if WK_GRU_FLAGS
+  // wait until waves base .. base + 3 have finished `v` steps (bounded: on a
+  // timeout the abort word is set, every later wait returns at once and the
+  // results are wrong, but the grid drains)
+  auto wait4 = [&](int base, unsigned v) {
+    auto ld = [&](int i) { return __hip_atomic_load(&gflags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    for (unsigned it = 0;; ++it) {
+      if (min(min(ld(base), ld(base + 1)), min(ld(base + 2), ld(base + 3))) >= v) break;
+      if ((it & 15) == 15 && (it > (1u << 22) || ld(8))) {
+        __hip_atomic_store(&gflags[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  };
+#endif
   auto step_body = [&](int step, f32x4 (&g)[2][3], f32x4 (&gn)[2][3], int slot) {
+#if WK_GRU_FLAGS
+    // slices 0-1 of the h-part (units 0-63) need only waves 0-3's state;
+    // the older waves start them while the younger finish the previous step
+    wait4(0, (unsigned)step);
+    f32x4 anh[2] = {b_hn, b_hn};
+    {
+      h8x hv0[2][2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) hv0[q][s] = *reinterpret_cast<const h8x*>(h16[cur] + (16 * q + n) * kGxHP + 8 * lg + 32 * s);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          g[q][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[s], hv0[q][s], g[q][0], 0, 0, 0);
+          g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wz[s], hv0[q][s], g[q][1], 0, 0, 0);
+          anh[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wn[s], hv0[q][s], anh[q], 0, 0, 0);
+        }
+    }
+    wait4(4, (unsigned)step);
+    stage_x(slot, step & 1);
+    store_y(cur, step - 1, step > 0);
+    load_x(slot, step + 2 + kXPf);
+    h8x hv[2][2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) hv[q][s] = *reinterpret_cast<const h8x*>(h16[cur] + (16 * q + n) * kGxHP + 8 * lg + 32 * (s + 2));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        g[q][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[s + 2], hv[q][s], g[q][0], 0, 0, 0);
+        g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wz[s + 2], hv[q][s], g[q][1], 0, 0, 0);
+        anh[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wn[s + 2], hv[q][s], anh[q], 0, 0, 0);
+      }
+#else
     // memory work of the step (independent of the MFMAs): x rows of step + 2
     // into the tile the previous step's x-part read, the previous step's
     // outputs (none at step 0), the ring slot refilled
@@ -1268,6 +1334,7 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
         g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wz[s], hv[q][s], g[q][1], 0, 0, 0);
         anh[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wn[s], hv[q][s], anh[q], 0, 0, 0);
       }
+#endif
     // gate math of both tiles (tile 0 beside tile 1's h-part, tile 1 beside
     // the x-part of the next step; the last step's x-part reads a stale tile
     // and is discarded)
@@ -1281,9 +1348,10 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
         o[q][i] = (_Float16)hn;
       }
     xpart((step + 1) & 1, gn);
-    __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);   // tile 0's h-part
+    constexpr int kHp = WK_GRU_FLAGS ? 6 : 12;           // h-part MFMAs per tile in this region
+    __builtin_amdgcn_sched_group_barrier(0x008, kHp, 0);  // tile 0's h-part
 #pragma unroll
-    for (int i = 0; i < 12; ++i) {                        // tile 1's h-part || tile 0's gates
+    for (int i = 0; i < kHp; ++i) {                       // tile 1's h-part || tile 0's gates
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, WK_GRU_VPM0, 0);
     }
@@ -1299,13 +1367,24 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
       if (!(WK_GRU_LDSABL & 8)) *reinterpret_cast<uint2*>(&h16[cur ^ 1][(16 * q + n) * kGxHP + u0]) = __builtin_bit_cast(uint2, o[q]);
     cur ^= 1;
     GRU_HIT(2);
+#if WK_GRU_FLAGS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's state slice, x-tile and output-copy LDS ops done
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (lane == 0) __hip_atomic_store(&gflags[wave], (unsigned)step + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#else
     __syncthreads();
+#endif
     GRU_HIT(3);
   };
   for (int step = 0; step < T; step += 2) {
     step_body(step, ga, gb, 0);
     if (step + 1 < T) step_body(step + 1, gb, ga, 1);
   }
+#if WK_GRU_FLAGS
+  wait4(0, (unsigned)T);   // every wave's last state slice is in the image
+  wait4(4, (unsigned)T);
+#endif
   store_y(cur, T - 1, true);   // the last step's outputs
 #ifdef WK_GRU_STAMPS
   if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0)
