@@ -1634,7 +1634,28 @@ __device__ unsigned long long g_out_stamps[kOutWaves][16];
 #else
 #define OUT_HIT(k) do {} while (0)
 #endif
-template <bool LOGITS>
+// KEYED (V <= 4096, so 4 NT <= 256): the running maximum carries its column
+// in the value's low 8 mantissa bits (the tag 255 - (4 tile + cf); the column
+// is 16 (4 tile + cf) + li), so the epilogue is one v_and_or_b32 per value and
+// one v_max3_f32 per two values instead of compare + two selects per value.
+// A tagged value moves by < 2^-15 of itself: the first maximum is exact except
+// between logits that agree to within that (fp16 operands already put ~1e-3 of
+// noise on every logit); the tokens stay a function of the row alone.
+#ifndef WK_OUT_KEYED
+#define WK_OUT_KEYED 1
+#endif
+// m = max(m, k0, k1) on the tagged values (fmaxf would first canonicalise
+// each of them: they come from integer ops).  The tags are applied in C++, so
+// the compiler still places the wait states for reading MFMA results.
+__device__ __forceinline__ float out_max3(float m, float k0, float k1) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(k0), "v"(k1));
+  return r;
+}
+__device__ __forceinline__ float out_tag(float x, unsigned mask, unsigned tag) {
+  return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, x) & mask) | tag);
+}
+template <bool LOGITS, bool KEYED>
 __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const __half* __restrict__ y,
                                                                           const __half* __restrict__ w,
                                                                           const float* __restrict__ bias, int64_t rows,
@@ -1731,6 +1752,8 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   __syncthreads();
   float mx[kOutRF][4];
   int ix[kOutRF][4];
+  unsigned kmask;   // (KEYED) 0xFFFFFF00 in a VGPR the compiler cannot fold: one v_and_or_b32
+  asm("v_mov_b32 %0, 0xffffff00" : "=v"(kmask));   // per tag (a literal mask would split it in two)
 #pragma unroll
   for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
@@ -1753,7 +1776,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #ifndef WK_OUT_DMA_SPREAD
 #define WK_OUT_DMA_SPREAD 0   // (measured -2 to -4 %, not kept) the leading waves' LDS-DMA pieces issued between the epilogue's column blocks
 #endif
-  auto epilogue_t = [&](int tile, auto full, int dma_tile) {
+  auto epilogue_t = [&](int tile, auto full, int dma_tile) __attribute__((always_inline)) {
     // column v = 64 tile + 16 cf + li, rows row0 + 16 rf + 4 lg + i
 #pragma unroll
     for (int cf = 0; cf < 4; ++cf) {
@@ -1764,7 +1787,31 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       }
 #endif
       const int v = tile * kOutBN + 16 * cf + li;
-      if (decltype(full)::value || v < V) {
+      if (KEYED) {
+        const unsigned tag = 255u - (unsigned)(4 * tile + cf);
+        if (LOGITS) {
+#pragma unroll
+          for (int rf = 0; rf < kOutRF; ++rf)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int64_t r = row0 + 16 * rf + 4 * lg + i;
+              if ((decltype(full)::value || v < V) && r < rows) logits[r * V + v] = __float2half(acc[rf][cf][i]);
+            }
+        }
+        if (cf & 1) {   // columns cf - 1 and cf: two tagged values per v_max3_f32
+#pragma unroll
+          for (int rf = 0; rf < kOutRF; ++rf)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              float x0 = acc[rf][cf - 1][i], x1 = acc[rf][cf][i];
+              if (!decltype(full)::value) {   // (-FLT_MAX: tagged -inf would be a NaN)
+                x0 = v - 16 < V ? x0 : -FLT_MAX;
+                x1 = v < V ? x1 : -FLT_MAX;
+              }
+              mx[rf][i] = out_max3(mx[rf][i], out_tag(x0, kmask, tag + 1), out_tag(x1, kmask, tag));
+            }
+        }
+      } else if (decltype(full)::value || v < V) {
 #pragma unroll
         for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
@@ -1779,7 +1826,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       }
     }
   };
-  auto epilogue = [&](int tile, int dma_tile = -1) {
+  auto epilogue = [&](int tile, int dma_tile = -1) __attribute__((always_inline)) {
     if ((tile + 1) * kOutBN <= V) epilogue_t(tile, std::true_type{}, dma_tile);
     else epilogue_t(tile, std::false_type{}, dma_tile);
   };
@@ -1847,7 +1894,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float m = mx[rf][i];
-      int k = ix[rf][i];
+      int k = KEYED ? 16 * (255 - (int)(__builtin_bit_cast(unsigned, m) & 255u)) + li : ix[rf][i];
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
         const float om = __shfl_xor(m, o, 64);
@@ -2215,13 +2262,13 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     const int nv = n_valid < n_samples ? n_valid : n_samples;
-    const int64_t passes = (rows + kFftFrames - 1) / kFftFrames;
-    const int64_t blocks = (passes + kFftWaves - 1) / kFftWaves;
     // n_valid == 0: every sample is padding; the kernel's (masked) loads then
     // read a device table instead of a possibly empty audio buffer
     const float* au = nv > 0 ? d_audio : c->fft_win;
     wk_status s = timed(c, WK_CTC_STAGE_LOGMEL, st, [&]() -> wk_status {
 #ifdef WK_LOGMEL_V1
+      const int64_t passes = (rows + kFftFrames - 1) / kFftFrames;
+      const int64_t blocks = (passes + kFftWaves - 1) / kFftWaves;
       hipLaunchKernelGGL(ctc_logmel_fft_kernel, dim3((unsigned)(blocks < 8 * c->n_cu ? blocks : 8 * c->n_cu)), dim3(256),
                          0, st, au, nv > 0 ? stride : (int64_t)0, nv, n_samples, T, rows, c->fft_win, c->fft_tw,
                          c->fb_start, c->fb_len, c->fb_off, c->fb_w, c->n_fbw, d_feats);
@@ -2338,14 +2385,16 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
       // fused output layer + argmax; fp16 logits are written only for log_softmax
       const dim3 og((unsigned)((rows + out_rows(d_log_probs != nullptr) - 1) / out_rows(d_log_probs != nullptr)));
       s = timed(c, WK_CTC_STAGE_OUTPUT, st, [&]() -> wk_status {
+        const bool keyed = WK_OUT_KEYED && V <= 64 * kOutBN;   // the tag holds 4 tile + cf in 8 bits
         if (d_log_probs) {
-          hipLaunchKernelGGL(ctc_out_argmax16_kernel<true>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
-                             c->out_b, rows, V, c->logits16, c->best);
+          hipLaunchKernelGGL((keyed ? ctc_out_argmax16_kernel<true, true> : ctc_out_argmax16_kernel<true, false>), og,
+                             dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, c->logits16, c->best);
           hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st,
                              c->logits16, c->zero_b, rows, V, d_log_probs, (int*)nullptr, (int)batch, T);   // bias already in
         } else {
-          hipLaunchKernelGGL(ctc_out_argmax16_kernel<false>, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16,
-                             c->out_b, rows, V, (__half*)nullptr, c->best);
+          hipLaunchKernelGGL((keyed ? ctc_out_argmax16_kernel<false, true> : ctc_out_argmax16_kernel<false, false>), og,
+                             dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, (__half*)nullptr,
+                             c->best);
         }
         return WK_OK;
       });

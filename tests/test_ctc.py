@@ -119,11 +119,12 @@ def test_ctc_fp16_gemm_mode(ctc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("vocab", [37, 100, 4000])
+@pytest.mark.parametrize("vocab", [37, 100, 4000, 4100])
 def test_ctc_fp16_ragged_vocab(vocab):
     """The fused fp16 output layer + argmax walks V in 64-column tiles: a
     vocabulary that is not a multiple of 64 (and a large one) must give the
-    oracle's decisions on confident frames, with and without log-probs."""
+    oracle's decisions on confident frames, with and without log-probs.
+    (V > 4096 takes the untagged compare-and-select epilogue.)"""
     import wakeword
     if not torch.cuda.is_available():
         pytest.skip("needs a HIP device")
