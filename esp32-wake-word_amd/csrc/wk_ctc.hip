@@ -1605,6 +1605,9 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef WK_OUT_PRIO
 #define WK_OUT_PRIO 0
 #endif
+#ifndef WK_OUT_BPIPE
+#define WK_OUT_BPIPE 0
+#endif
 #ifndef WK_OUT_AGPR
 #define WK_OUT_AGPR 0
 #endif
@@ -1842,12 +1845,32 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     const _Float16* b = bt[nt & 1];
     if (lag && nt > 0) epilogue(nt - 1);
     OUT_HIT(0);
+#if WK_OUT_BPIPE
+    // B fragments one k-step ahead: step st + 1's four reads are issued
+    // before step st's MFMAs (the compiler otherwise slots them among the last
+    // MFMAs of the step, ~1-4 MFMAs before their use)
+    h8 bfp[2][4];
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf)
+      bfp[0][cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, lg));
+#endif
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
+#if WK_OUT_BPIPE
+      if (st + 1 < 8) {
+#pragma unroll
+        for (int cf = 0; cf < 4; ++cf)
+          bfp[(st + 1) & 1][cf] =
+              *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, 4 * (st + 1) + lg));
+      }
+      __builtin_amdgcn_sched_barrier(0);   // the next step's reads stay ahead of this step's MFMAs
+      const h8* bf = bfp[st & 1];
+#else
       h8 bf[4];
 #pragma unroll
       for (int cf = 0; cf < 4; ++cf)
         bf[cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, 4 * st + lg));
+#endif
       if (st == 0) {
 #pragma unroll
         for (int cf = 0; cf < 4; ++cf) {
@@ -1863,6 +1886,9 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
           for (int cf = 0; cf < 4; ++cf)
             acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf[cf], acc[rf][cf], 0, 0, 0);
       }
+#if WK_OUT_BPIPE
+      __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     OUT_HIT(1);
 #if WK_OUT_DMA
