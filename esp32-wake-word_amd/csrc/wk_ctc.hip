@@ -32,6 +32,8 @@
 
 #include <math.h>
 #include <type_traits>
+#include <functional>
+#include <algorithm>
 #include <vector>
 
 #include <hip/hip_fp16.h>
@@ -1932,6 +1934,85 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     }
 }
 
+// Window starts of ctc_logmel_fft2_kernel's straight-line filterbank.  A tap
+// is a ds_read_b64 of the pair-power row at bin ws[lane] + j, served 32 lanes
+// at a time: two lanes of a half-wave share banks when their starts differ by
+// a nonzero multiple of 32 bins.  A filter shorter than its window can start
+// up to (window - length) bins early (the extra taps weigh 0), so the starts
+// are chosen with distinct residues mod 32 per half-wave where possible
+// (equal starts are free: one address is a broadcast).  Set 1: mel l over
+// kMelW1 bins; set 2 (lanes 0-31): mel 64 + l / 2 split at cut[l] between two
+// kMelW2-bin windows.  A half-wave without a solution keeps the natural starts.
+void pick_mel_windows(const std::vector<int>& st, const std::vector<int>& ln, std::vector<int>& ws, std::vector<int>& cut) {
+  auto conflict_free = [](const int* w, int n) {
+    for (int a = 0; a < n; ++a)
+      for (int b = a + 1; b < n; ++b)
+        if (w[a] != w[b] && (w[a] - w[b]) % 32 == 0) return false;
+    return true;
+  };
+  // set 1, per half-wave: bipartite matching of lanes to residues
+  for (int h = 0; h < 2; ++h) {
+    int* w = &ws[32 * h];
+    for (int l = 0; l < 32; ++l) w[l] = std::min(st[32 * h + l], kBins - kMelW1);
+    if (conflict_free(w, 32)) continue;
+    int owner[32], pick[32];
+    std::fill(owner, owner + 32, -1);
+    std::function<bool(int, unsigned&)> aug = [&](int l, unsigned& seen) -> bool {
+      const int m = 32 * h + l, hi = std::min(st[m], kBins - kMelW1), lo = std::max(0, st[m] + ln[m] - kMelW1);
+      for (int s = hi; s >= lo; --s) {
+        const int r = s & 31;
+        if (seen >> r & 1u) continue;
+        seen |= 1u << r;
+        if (owner[r] < 0 || aug(owner[r], seen)) { owner[r] = l; pick[l] = s; return true; }
+      }
+      return false;
+    };
+    bool ok = true;
+    for (int l = 0; l < 32 && ok; ++l) { unsigned seen = 0; ok = aug(l, seen); }
+    if (ok)
+      for (int l = 0; l < 32; ++l) w[l] = pick[l];
+  }
+  // set 2: per mel a pair (h0, h1); the cut is h0 + kMelW2.  Depth-first,
+  // most constrained mel first, with a node budget (then natural starts)
+  int sol[16][2], order[16], nopt[16];
+  std::vector<std::pair<int, int>> opts[16];
+  for (int p = 0; p < 16; ++p) {
+    const int m = 64 + p;
+    for (int h0 = std::max(0, st[m] + ln[m] - 2 * kMelW2); h0 <= st[m]; ++h0)
+      for (int h1 = std::max(h0, st[m] + ln[m] - kMelW2); h1 <= std::min(h0 + kMelW2, kBins - kMelW2); ++h1)
+        if ((h0 & 31) != (h1 & 31)) opts[p].push_back({h0, h1});
+    nopt[p] = (int)opts[p].size();
+    order[p] = p;
+  }
+  std::stable_sort(order, order + 16, [&](int a, int b) { return nopt[a] < nopt[b]; });
+  unsigned used = 0;
+  long budget = 1 << 20;
+  std::function<bool(int)> bt = [&](int d) -> bool {
+    if (d == 16) return true;
+    const int p = order[d];
+    for (const auto& o : opts[p]) {
+      if (--budget < 0) return false;
+      const unsigned bits = (1u << (o.first & 31)) | (1u << (o.second & 31));
+      if (used & bits) continue;
+      used |= bits;
+      sol[p][0] = o.first;
+      sol[p][1] = o.second;
+      if (bt(d + 1)) return true;
+      used &= ~bits;
+    }
+    return false;
+  };
+  const bool ok2 = bt(0);
+  for (int l = 0; l < 32; ++l) {
+    const int m = 64 + l / 2;
+    const int h0 = ok2 ? sol[l / 2][0] : std::min(st[m], kBins - kMelW2);
+    const int h1 = ok2 ? sol[l / 2][1] : std::min(st[m] + kMelW2, kBins - kMelW2);
+    ws[64 + l] = (l & 1) ? h1 : h0;
+    cut[64 + l] = (l & 1) ? kBins : std::min(h0 + kMelW2, h1 + kMelW2);
+  }
+  // (lanes 32-63 of set 2 carry zero weights and all read bin 0: a broadcast)
+}
+
 // HTK mel filterbank of torchaudio.functional.melscale_fbanks(201, 0, 8000, 80, 16000), in fp32 like torch.
 void mel_fbank(std::vector<float>& fb) {
   fb.assign((size_t)kBins * kMels, 0.0f);
@@ -2230,26 +2311,39 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     {   // straight-line windows of ctc_logmel_fft2_kernel (see there)
       std::vector<float> mw((size_t)64 * (kMelW1 + kMelW2), 0.0f);
       std::vector<int> ws(128, 0);
-      auto window = [&](int m, int wdt, int first, int lanes_w, float* dst, int* wsd) {
-        // window of wdt bins inside [0, kBins) covering the filter from bin `first`
-        int w0 = st[m] + first;
-        if (w0 + wdt > kBins) w0 = kBins - wdt;
-        *wsd = w0;
-        for (int j = 0; j < lanes_w; ++j) {
-          const int k = w0 + j;
-          const bool mine = k >= st[m] + first && k < st[m] + first + wdt && k <= st[m] + ln[m] - 1;
-          dst[j] = mine ? 0.25f * fb[(size_t)k * kMels + m] : 0.0f;
-        }
-      };
+      std::vector<int> cut(128, kBins);   // (second set) a lane takes filter bins in [ws, cut)
       bool fits = kMels == 80;
-      for (int m = 0; m < 64 && fits; ++m) {
-        fits = ln[m] <= kMelW1;
-        window(m, kMelW1, 0, kMelW1, &mw[(size_t)m * kMelW1], &ws[m]);
-      }
-      for (int l = 0; l < 32 && fits; ++l) {
-        const int m = 64 + l / 2;
-        fits = ln[m] <= 2 * kMelW2;
-        window(m, kMelW2, (l & 1) * kMelW2, kMelW2, &mw[(size_t)64 * kMelW1 + (size_t)l * kMelW2], &ws[64 + l]);
+      for (int m = 0; m < 64 && fits; ++m) fits = ln[m] <= kMelW1;
+      for (int m = 64; m < kMels && fits; ++m) fits = ln[m] <= 2 * kMelW2;
+      if (fits) {
+        pick_mel_windows(st, ln, ws, cut);
+        for (int m = 0; m < 64; ++m)
+          for (int j = 0; j < kMelW1; ++j) {
+            const int k = ws[m] + j;
+            const bool mine = k >= st[m] && k < st[m] + ln[m];
+            mw[(size_t)m * kMelW1 + j] = mine ? 0.25f * fb[(size_t)k * kMels + m] : 0.0f;
+          }
+        for (int l = 0; l < 32; ++l) {
+          const int m = 64 + l / 2;
+          for (int j = 0; j < kMelW2; ++j) {
+            const int k = ws[64 + l] + j;
+            const bool mine = k >= st[m] && k < st[m] + ln[m] && k < cut[64 + l] && ((l & 1) == 0 || k >= cut[64 + l - 1]);
+            mw[(size_t)64 * kMelW1 + (size_t)l * kMelW2 + j] = mine ? 0.25f * fb[(size_t)k * kMels + m] : 0.0f;
+          }
+        }
+        // every filter tap lands in exactly one window
+        for (int m = 0; m < kMels && fits; ++m) {
+          int taps = 0;
+          if (m < 64) {
+            for (int j = 0; j < kMelW1; ++j) taps += mw[(size_t)m * kMelW1 + j] != 0.0f;
+          } else {
+            for (int h = 0; h < 2; ++h)
+              for (int j = 0; j < kMelW2; ++j) taps += mw[(size_t)64 * kMelW1 + (size_t)(2 * (m - 64) + h) * kMelW2 + j] != 0.0f;
+          }
+          int nz = 0;
+          for (int k = st[m]; k < st[m] + ln[m]; ++k) nz += fb[(size_t)k * kMels + m] != 0.0f;
+          fits = taps == nz;
+        }
       }
       if (e == hipSuccess && !fits) e = hipErrorInvalidValue;
       if (e == hipSuccess) e = upload(&c->melw, mw.data(), mw.size());
