@@ -4,7 +4,9 @@ B utterances of 3 s (48,000 samples, T = 301 frames at hop 160), synthetic
 (device generator), seeded GRU_CTC_Model weights (the reference ships none),
 fixed V.  One step = log-mel front-end + encoder + 2-layer BiGRU + output
 layer + argmax + greedy decode, inputs resident in HBM and the token
-sequences left there (CTCModel.decode; forward() adds the host list form).
+sequences left there: one wk_ctc_transcribe call (CTCModel.decode_audio; in
+fp16 mode the z-score is folded into the encoder), or with --separate the
+reference's two steps, wk_ctc_features then wk_ctc_forward.
 
 Prints one JSON line: utterances/s over the timed steps, and per stage (HIP
 events on the launch stream, wk_ctc_profile) the mean duration with its
@@ -30,7 +32,7 @@ STAGES = ["logmel", "zscore", "encoder", "proj0", "gru0", "proj1", "gru1", "outp
 H, MELS = 128, 80
 
 
-def stage_work(B, T, V, n_samples, f16):
+def stage_work(B, T, V, n_samples, f16, zfold=False):
     """(algorithmic HBM bytes, algorithmic flop) per launch of each stage (the
     compulsory reads and writes of its inputs and outputs; weights, read once
     through L2, are counted once)."""
@@ -39,7 +41,8 @@ def stage_work(B, T, V, n_samples, f16):
     gi = 2 if f16 else 4
     out = {
         "logmel": (B * n_samples * 4 + rows * MELS * 4, rows * 4600 + rows * MELS * 2 * 6),
-        "zscore": (2 * rows * MELS * 4, rows * MELS * 5),
+        # (zfold: only the per-utterance statistics from the log-mel passes' partials)
+        "zscore": ((rows + 5) // 6 * 16 + B * 8, B * 4 * ((T + 5) // 6 + 1)) if zfold else (2 * rows * MELS * 4, rows * MELS * 5),
         "encoder": (rows * MELS * 4 + rows * H * a + (H * MELS) * 4, rows * H * MELS * 2),
         "proj0": (rows * H * a + rows * 6 * H * gi + 6 * H * H * a, rows * 6 * H * H * 2),
         "gru0": (rows * 6 * H * gi + rows * 2 * H * a, rows * 2 * 3 * H * H * 2),
@@ -77,6 +80,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16"],
                     help="GEMM operand precision (config 5 names fp16; fp32 is the parity mode)")
+    ap.add_argument("--separate", action="store_true",
+                    help="time wk_ctc_features + wk_ctc_forward instead of the one-call wk_ctc_transcribe")
     args = ap.parse_args()
     import torch
     import wakeword
@@ -90,14 +95,21 @@ def main():
     m = CO.make_model(V, seed=0)
     g = wakeword.CTCModel(m.state_dict(), V, precision=args.precision)
     audio = wakeword.synth_clips(1234, 0, B, n)
+    if args.separate:
+        def step():
+            tok, ln, _ = g.decode(g.features(audio, n_samples=n))
+            return tok, ln
+    else:
+        def step():
+            return g.decode_audio(audio, n_samples=n)
     for _ in range(args.warmup):
-        g.decode(g.features(audio, n_samples=n))
+        step()
     torch.cuda.synchronize()
 
     # timed region: the whole step, host clock, no per-stage events
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        tok, ln, _ = g.decode(g.features(audio, n_samples=n))
+        tok, ln = step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     value = B * args.steps / el
@@ -107,12 +119,13 @@ def main():
     L = _lib.lib()
     _lib.check(L.wk_ctc_profile(g._h, 1), "wk_ctc_profile")
     for _ in range(args.steps):
-        g.decode(g.features(audio, n_samples=n))
+        step()
     ms = (C.c_double * len(STAGES))()
     cnt = (C.c_int64 * len(STAGES))()
     _lib.check(L.wk_ctc_stage_times(g._h, ms, cnt), "wk_ctc_stage_times")
     _lib.check(L.wk_ctc_profile(g._h, 0), "wk_ctc_profile")
-    work = stage_work(B, T, V, n, f16)
+    zfold = f16 and not args.separate and T >= 6
+    work = stage_work(B, T, V, n, f16, zfold)
     fused = f16 and cnt[STAGES.index("proj0")] == 0
     if fused:
         # projection fused into the recurrence: the layer reads its input rows
@@ -148,7 +161,9 @@ def main():
         "dtype": "f32" if not f16 else "f16 GEMM/MFMA operands, f32 accumulate, f32 gate math and front-end",
         "data": "synthetic (device generator), seeded GRU_CTC_Model weights (the reference ships none)",
         "config": {"workload": "config5: CTC head, 3 s utterances", "batch": B, "vocab": V, "T": T,
-                   "precision": args.precision},
+                   "precision": args.precision,
+                   "call": "wk_ctc_features + wk_ctc_forward" if args.separate else "wk_ctc_transcribe"
+                   + (" (z-score folded into the encoder)" if zfold else "")},
         "roofline": {"kernel": dom, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
                      "unit": d["unit"], "frac": d["frac"], "traffic": d["traffic"]},
         "kernels": kernels,

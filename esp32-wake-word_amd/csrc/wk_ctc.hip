@@ -298,13 +298,29 @@ struct CtcFft2Lds {
   f2 w[kF2Waves][kF2Pairs * 20 * kA2Pitch];   // per wave: A, then the exchange, then the power rows
 };
 
+// STATS (wk_ctc_transcribe, fp16 mode, T >= 6): the features stay un-normalised
+// and each pass also leaves part[ps] = {S0, Q0, S1, Q1}: the sums of (x - K) and
+// (x - K)^2 over its rows' log-mel values x, split between the utterance of the
+// pass's first row (0) and the next one (1), with K = ln(1e-8) the floor of x
+// (so a silent utterance sums to exactly 0).  ctc_zstats_kernel folds them into
+// each utterance's mean and 1/std, which the encoder applies as it loads.
+__device__ __forceinline__ float row16_sum(float v) {   // every lane: the sum over its 16-lane row (DPP)
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+  return v;
+}
+__device__ __forceinline__ float sum_rows4(float v);
+template <bool STATS>
 __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const float* __restrict__ audio, int64_t stride,
                                                                             int n_valid, int n_pad, int T, int64_t rows,
                                                                             const float* __restrict__ win_g,
                                                                             const float* __restrict__ tw_g,
                                                                             const float* __restrict__ melw,
                                                                             const int* __restrict__ melws,
-                                                                            float* __restrict__ feats) {
+                                                                            float* __restrict__ feats,
+                                                                            float4* __restrict__ part) {
   __shared__ CtcFft2Lds L;
   constexpr int NT = kF2Waves * 64;
   for (int i = threadIdx.x; i < kNfft; i += NT) L.win[i] = win_g[i];
@@ -350,12 +366,14 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
   };
   // both frames of the lane group's pair: one division for frame a, frame b is
   // the next row (t + 1, or frame 0 of the next utterance)
+  int ta_next = 0;
   auto load_pair = [&](int64_t ps_, float (&ra_)[20], float (&rb_)[20]) {
     const int64_t row = ps_ * kRowsPerPass + 2 * g;
     const bool live_a = g < kF2Pairs && ps_ < passes && row < rows;
     const bool live_b = live_a && row + 1 < rows;
     const int rr = live_a ? (int)row : 0;   // rows < 2^31 (host check)
     const int ba = (int)((unsigned)rr / (unsigned)T), ta = rr - ba * T;
+    ta_next = __builtin_amdgcn_readfirstlane(ta);   // lane 0: the pass's first row (STATS)
     const bool wrap = ta + 1 == T;
     load_one(live_a, ba, ta, ra_);
     load_one(live_b, wrap ? ba + 1 : ba, wrap ? 0 : ta + 1, rb_);
@@ -372,6 +390,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
   load_pair((int64_t)blockIdx.x * kF2Waves + wv, ra, rb);
   const bool lact = g < kF2Pairs;
   for (int64_t ps = (int64_t)blockIdx.x * kF2Waves + wv; ps < passes; ps += pstep) {
+    const int ta_cur = ta_next;   // frame index of this pass's first row in its utterance
     // stage 1: lane (g, n2 = q): DFT-20 over n1 of z[20 n1 + n2] = w (x_a + i x_b)
     f2 v[20];
 #pragma unroll
@@ -468,12 +487,54 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
       const float av[6] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y};
       const bool half0 = lane < 2 * (kMels - 64) && (lane & 1) == 0;
       const int o2 = half0 ? 4 * (64 + (lane >> 1)) : 0x40000000;
+      float la[6], lc[6];
 #pragma unroll
       for (int f = 0; f < 6; ++f) {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, wk_logf(av[f] + 1e-8f)), fr,
-                                              4 * (f * kMels + lane), 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, wk_logf(cv[f] + 1e-8f)), fr,
-                                              o2 + 4 * f * kMels, 0, 0);
+        la[f] = wk_logf(av[f] + 1e-8f);
+        lc[f] = wk_logf(cv[f] + 1e-8f);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, la[f]), fr, 4 * (f * kMels + lane), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, lc[f]), fr, o2 + 4 * f * kMels, 0, 0);
+      }
+      if constexpr (STATS) {
+        // rows r0 .. r0 + nr - 1; those from bnd on belong to the next utterance
+        const int bnd = T - ta_cur;
+        const float m2 = half0 ? 1.0f : 0.0f;   // the second filter set counts once per mel (even lanes 0-30)
+        const float kLogFloor = wk_logf(1e-8f);   // bit-identical to a silent bin's value
+        // per frame P = {x - K, (y - K) m2} for the lane's two filters; sums {Sx, Sy}, {Qx, Qy}
+        f2 s0 = {0.0f, 0.0f}, q0 = {0.0f, 0.0f}, s1 = {0.0f, 0.0f}, q1 = {0.0f, 0.0f};
+        const f2 pm = {1.0f, m2}, pk = {-kLogFloor, -kLogFloor * m2};
+        if (bnd >= 6 && nr == 6) {   // the common pass: one utterance, all rows live
+#pragma unroll
+          for (int f = 0; f < 6; ++f) {
+            const f2 P = fma2(f2{la[f], lc[f]}, pm, pk);
+            s0 = s0 + P;
+            q0 = fma2(P, P, q0);
+          }
+        } else {
+#pragma unroll
+          for (int f = 0; f < 6; ++f) {
+            const f2 P = fma2(f2{la[f], lc[f]}, pm, pk);
+            if (f < nr) {   // wave-uniform
+              if (f < bnd) {
+                s0 = s0 + P;
+                q0 = fma2(P, P, q0);
+              } else {
+                s1 = s1 + P;
+                q1 = fma2(P, P, q1);
+              }
+            }
+          }
+        }
+        const f2 sq0 = {s0.x + s0.y, q0.x + q0.y}, sq1 = {s1.x + s1.y, q1.x + q1.y};
+        float t[4] = {sq0.x, sq0.y, sq1.x, sq1.y};
+        const int nred = bnd < nr ? 4 : 2;   // wave-uniform: slot 1 is empty unless the pass straddles
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i < nred) t[i] = sum_rows4(row16_sum(t[i]));
+        const __amdgpu_buffer_rsrc_t prs = make_rsrc(part + ps, 16u);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
+                                                                  make_float4(t[0], t[1], t[2], t[3])),
+                                               prs, lane == 0 ? 0 : 0x40000000, 0, 0);
       }
     }
     wave_lds_sync();
@@ -562,6 +623,35 @@ __global__ __launch_bounds__(1024) void ctc_zscore_kernel(float* __restrict__ fe
   if (!(sd > 0.0f)) return;
   const float inv = 1.0f / sd;
   for (int64_t i = tid; i < n_per; i += 1024) f[i] = (f[i] - mean) * inv;
+}
+
+// The z-score's statistics for wk_ctc_transcribe: one wave per utterance
+// folds the log-mel passes' {S, Q} partials (ctc_logmel_fft2_kernel<true>) in
+// double into zs[b] = {mean, 1/std} (unbiased std, ctc.py:101-104), or {0, 1}
+// when std is 0 (no normalisation).  Needs T >= 6: a pass then spans at most
+// two utterances.
+__global__ __launch_bounds__(256) void ctc_zstats_kernel(const float4* __restrict__ part, int64_t batch, int T,
+                                                         float2* __restrict__ zs) {
+  // one wave per utterance: lane i takes passes p0 + i, + 64, ...
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= batch) return;   // (wave-uniform)
+  const int64_t r0 = b * T, p0 = r0 / 6, p1 = (r0 + T - 1) / 6;
+  double S = 0.0, Q = 0.0;
+  for (int64_t p = p0 + lane; p <= p1; p += 64) {
+    const float4 v = part[p];
+    const bool first = 6 * p >= r0;   // the pass starts in this utterance (slot 0), else it is the pass's slot 1
+    S += first ? v.x : v.z;
+    Q += first ? v.y : v.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    S += __shfl_xor(S, o, 64);
+    Q += __shfl_xor(Q, o, 64);
+  }
+  const double n = (double)T * kMels, m = S / n, var = (Q - S * m) / (n - 1.0);
+  const float sd = var > 0.0 ? (float)sqrt(var) : 0.0f;
+  if (lane == 0) zs[b] = sd > 0.0f ? make_float2(wk_logf(1e-8f) + (float)m, 1.0f / sd) : make_float2(0.0f, 1.0f);
 }
 
 // ---------------------------------------------------------------------------
@@ -661,11 +751,14 @@ typedef _Float16 h8e __attribute__((ext_vector_type(8)));
 // Output rows are time-major (row t B + b for input row b T + t): the fp16
 // path keeps every [rows][.] tensor after the encoder in that order, so that a
 // GRU step's 16 utterances are 16 adjacent rows of the gate inputs and outputs.
+// NORM (wk_ctc_transcribe): the input rows are raw log-mel; each is z-scored
+// with its utterance's zs = {mean, 1/std} (ctc_zstats_kernel) as it is loaded.
+template <bool NORM>
 __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restrict__ in, int64_t rows,
                                                             const float* __restrict__ w, const float* __restrict__ bias,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, int B, int T,
-                                                            __half* __restrict__ out) {
+                                                            const float2* __restrict__ zs, __half* __restrict__ out) {
   constexpr int KS = 3, CT = kH / 16;
   __shared__ __attribute__((aligned(16))) h8e wf[KS][CT][64];   // A[col 16 ct + (l&15)][k = 32 s + 8 (l>>4) + j]
   __shared__ __attribute__((aligned(16))) float pb[3][kH];      // bias, gamma, beta
@@ -710,12 +803,25 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
   load_blk(blk);
   for (; blk < nblk; blk += (int64_t)gridDim.x * 4) {
     const int64_t r = blk * 16 + li;   // this lane's row
+    const int rr = r < rows ? (int)r : 0;   // rows < 2^31 (host check)
+    const int ub = rr / T, ut = rr - ub * T;
     h8e xb[KS];
+    if constexpr (NORM) {
+      const float2 z = zs[ub];
 #pragma unroll
-    for (int st = 0; st < KS; ++st) {
-      const float4 a = xr[st][0], b = xr[st][1];
-      xb[st] = h8e{(_Float16)a.x, (_Float16)a.y, (_Float16)a.z, (_Float16)a.w,
-                   (_Float16)b.x, (_Float16)b.y, (_Float16)b.z, (_Float16)b.w};
+      for (int st = 0; st < KS; ++st) {
+        const float4 a = xr[st][0], b = xr[st][1];
+        xb[st] = h8e{(_Float16)((a.x - z.x) * z.y), (_Float16)((a.y - z.x) * z.y), (_Float16)((a.z - z.x) * z.y),
+                     (_Float16)((a.w - z.x) * z.y), (_Float16)((b.x - z.x) * z.y), (_Float16)((b.y - z.x) * z.y),
+                     (_Float16)((b.z - z.x) * z.y), (_Float16)((b.w - z.x) * z.y)};
+      }
+    } else {
+#pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        const float4 a = xr[st][0], b = xr[st][1];
+        xb[st] = h8e{(_Float16)a.x, (_Float16)a.y, (_Float16)a.z, (_Float16)a.w,
+                     (_Float16)b.x, (_Float16)b.y, (_Float16)b.z, (_Float16)b.w};
+      }
     }
     load_blk(blk + (int64_t)gridDim.x * 4);   // the next block (past the end: zeros, unused)
     f32x4 acc[CT];
@@ -744,8 +850,6 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
       }
     s2 = sum_rows4(s2);
     const float rs = 1.0f / sqrtf(s2 * (1.0f / kH) + 1e-5f);   // biased variance, as nn.LayerNorm
-    const int rr = r < rows ? (int)r : 0;   // rows < 2^31 (host check)
-    const int ub = rr / T, ut = rr - ub * T;
     const int orow = r < rows ? (ut * B + ub) * (kH * 2) : 0x7FFFFE00;   // time-major output row (bytes); past the end: dropped
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
@@ -2068,6 +2172,10 @@ struct wk_ctc {
   float *x0, *gi, *y0, *y1, *logits;
   __half *x0h, *y0h, *y1h, *logits16;
   int* best;
+  float* tr_feats;      // wk_ctc_transcribe: [rows][80] features (raw in fp16 mode), pass partials, per-utterance z-score
+  float4* tr_part;
+  float2* tr_zs;
+  size_t tr_rows, tr_batch;
   int64_t last_batch;   // geometry of the last wk_ctc_forward (wk_ctc_frame_argmax)
   int32_t last_T;
   // stage timing (wk_ctc_profile): events recorded around each stage on the
@@ -2088,7 +2196,7 @@ int64_t ctc_num_weights(const wk_ctc_config* c) {
   return n + V * 2 * H + V;
 }
 
-void free_ws(wk_ctc* c) {
+void free_ws(wk_ctc* c) {   // (wk_ctc_forward's workspace; the transcribe buffers go in free_all)
   void* ps[] = {c->x0, c->gi, c->y0, c->y1, c->logits, c->best, c->x0h, c->y0h, c->y1h, c->logits16};
   for (void* q : ps) (void)hipFree(q);
   c->x0 = c->gi = c->y0 = c->y1 = c->logits = nullptr;
@@ -2139,6 +2247,8 @@ wk_status timed(wk_ctc* c, int stage, hipStream_t st, F launch) {
 void free_all(wk_ctc* c) {
   (void)fold_events(c);
   free_ws(c);
+  void* ts[] = {c->tr_feats, c->tr_part, c->tr_zs};
+  for (void* q : ts) (void)hipFree(q);
   void* ps[] = {c->enc_w, c->enc_b, c->ln_g, c->ln_b, c->wih[0], c->wih[1], c->bih[0], c->bih[1], c->bhh[0],
                 c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->zero_b, c->fb_w, c->wih16[0], c->wih16[1],
                 c->out_w16, c->fft_win, c->fft_tw, c->fb_start, c->fb_len, c->fb_off, c->whh16_pk[0], c->whh16_pk[1],
@@ -2369,8 +2479,11 @@ wk_status wk_ctc_destroy(wk_ctc* c) {
   });
 }
 
-wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n_valid, int32_t n_samples,
-                          int64_t stride, float* d_feats, void* stream) {
+namespace {
+// wk_ctc_features; with `part` (wk_ctc_transcribe, T >= 6) the features stay
+// raw and the z-score's statistics go to zs instead of being applied in place.
+wk_status ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n_valid, int32_t n_samples,
+                       int64_t stride, float* d_feats, void* stream, float4* part, float2* zs) {
   if (!c || batch < 0 || (batch > 0 && (!d_audio || !d_feats)) || n_samples < kNfft / 2 + 1 || n_valid < 0 ||
       (batch > 1 && stride < (n_valid < n_samples ? n_valid : n_samples)))
     return invalid("wk_ctc_features: bad arguments (n_samples must exceed 200 for the reflect pad)");
@@ -2395,15 +2508,22 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
 #else
       const int64_t passes2 = (rows + 2 * kF2Pairs - 1) / (2 * kF2Pairs);
       const int64_t blocks2 = (passes2 + kF2Waves - 1) / kF2Waves;
-      hipLaunchKernelGGL(ctc_logmel_fft2_kernel, dim3((unsigned)(blocks2 < c->n_cu ? blocks2 : c->n_cu)), dim3(kF2Waves * 64),
-                         0, st, au, nv > 0 ? stride : (int64_t)0, nv, n_samples, T, rows, c->fft_win, c->fft_tw,
-                         c->melw, c->melws, d_feats);
+      const dim3 lg2((unsigned)(blocks2 < c->n_cu ? blocks2 : c->n_cu));
+      if (part)
+        hipLaunchKernelGGL(ctc_logmel_fft2_kernel<true>, lg2, dim3(kF2Waves * 64), 0, st, au, nv > 0 ? stride : (int64_t)0,
+                           nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->melw, c->melws, d_feats, part);
+      else
+        hipLaunchKernelGGL(ctc_logmel_fft2_kernel<false>, lg2, dim3(kF2Waves * 64), 0, st, au, nv > 0 ? stride : (int64_t)0,
+                           nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->melw, c->melws, d_feats, (float4*)nullptr);
 #endif
       return WK_OK;
     });
     if (s == WK_OK)
       s = timed(c, WK_CTC_STAGE_ZSCORE, st, [&]() -> wk_status {
-        hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
+        if (part)
+          hipLaunchKernelGGL(ctc_zstats_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, part, batch, T, zs);
+        else
+          hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
         return WK_OK;
       });
     if (s != WK_OK) return s;
@@ -2412,8 +2532,10 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
   });
 }
 
-wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T, float* d_log_probs,
-                         int32_t* d_tokens, int32_t* d_lengths, void* stream) {
+// wk_ctc_forward; with zs (wk_ctc_transcribe, fp16 mode) the encoder z-scores
+// the raw feature rows as it loads them.
+wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T, float* d_log_probs, int32_t* d_tokens,
+                      int32_t* d_lengths, void* stream, const float2* zs) {
   if (!c || batch < 0 || T < 1 || (batch > 0 && (!d_feats || !d_tokens || !d_lengths)))
     return invalid("wk_ctc_forward: bad arguments");
   if (batch == 0) return WK_OK;
@@ -2452,9 +2574,13 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
 #endif
     const int enc_grid = (int)((rows + 63) / 64 < WK_ENC_GRID * c->n_cu ? (rows + 63) / 64 : WK_ENC_GRID * c->n_cu);
     wk_status s = timed(c, WK_CTC_STAGE_ENCODER, st, [&]() -> wk_status {
-      if (f16)
-        hipLaunchKernelGGL(ctc_encoder16_kernel, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w, c->enc_b,
-                           c->ln_g, c->ln_b, (int)batch, T, c->x0h);   // fp16 path: time-major rows from here on
+      if (f16 && zs)
+        hipLaunchKernelGGL(ctc_encoder16_kernel<true>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
+                           c->enc_b, c->ln_g, c->ln_b, (int)batch, T, zs, c->x0h);
+      else if (f16)
+        hipLaunchKernelGGL(ctc_encoder16_kernel<false>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
+                           c->enc_b, c->ln_g, c->ln_b, (int)batch, T, (const float2*)nullptr,
+                           c->x0h);   // fp16 path: time-major rows from here on
       else
         hipLaunchKernelGGL(ctc_encoder_kernel<float>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
                            c->enc_b, c->ln_g, c->ln_b, c->x0);
@@ -2550,6 +2676,53 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
     if (s != WK_OK) return s;
     e = hipGetLastError();
     return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_forward launch");
+  });
+}
+}  // namespace
+
+wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n_valid, int32_t n_samples,
+                          int64_t stride, float* d_feats, void* stream) {
+  return ctc_features(c, d_audio, batch, n_valid, n_samples, stride, d_feats, stream, nullptr, nullptr);
+}
+
+wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T, float* d_log_probs,
+                         int32_t* d_tokens, int32_t* d_lengths, void* stream) {
+  return ctc_forward(c, d_feats, batch, T, d_log_probs, d_tokens, d_lengths, stream, nullptr);
+}
+
+wk_status wk_ctc_transcribe(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n_valid, int32_t n_samples,
+                            int64_t stride, int32_t* d_tokens, int32_t* d_lengths, void* stream) {
+  if (!c || batch < 0 || n_samples < kNfft / 2 + 1 || (batch > 0 && (!d_tokens || !d_lengths)))
+    return invalid("wk_ctc_transcribe: bad arguments");
+  if (batch == 0) return WK_OK;
+  const int T = 1 + n_samples / kHop;
+  const int64_t rows = batch * (int64_t)T;
+  if (rows > INT32_MAX) return invalid("wk_ctc_transcribe: batch x frames exceeds 2^31 rows");
+  const bool fused = c->f16 && T >= 6;   // (a log-mel pass of 6 rows then spans at most two utterances)
+  return on_device(c->cfg.device, [&]() -> wk_status {
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    const int64_t passes = (rows + 5) / 6;
+    if ((size_t)rows > c->tr_rows || (size_t)batch > c->tr_batch) {   // grows on first use, then reused
+      if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
+      (void)hipFree(c->tr_feats);
+      (void)hipFree(c->tr_part);
+      (void)hipFree(c->tr_zs);
+      c->tr_feats = nullptr;
+      c->tr_part = nullptr;
+      c->tr_zs = nullptr;
+      c->tr_rows = c->tr_batch = 0;
+      if ((e = hipMalloc(&c->tr_feats, sizeof(float) * rows * kMels)) != hipSuccess ||
+          (e = hipMalloc(&c->tr_part, sizeof(float4) * passes)) != hipSuccess ||
+          (e = hipMalloc(&c->tr_zs, sizeof(float2) * batch)) != hipSuccess)
+        return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_ctc_transcribe workspace");
+      c->tr_rows = (size_t)rows;
+      c->tr_batch = (size_t)batch;
+    }
+    wk_status s = ctc_features(c, d_audio, batch, n_valid, n_samples, stride, c->tr_feats, stream,
+                               fused ? c->tr_part : nullptr, fused ? c->tr_zs : nullptr);
+    if (s != WK_OK) return s;
+    return ctc_forward(c, c->tr_feats, batch, T, nullptr, d_tokens, d_lengths, stream, fused ? c->tr_zs : nullptr);
   });
 }
 

@@ -31,7 +31,7 @@ EXPORTS = ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_syn
            "wk_ctc_num_weights", "wk_ctc_create", "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward",
            "wk_wav_read", "wk_wav_load_batch", "wk_augment", "flow_extract_mfcc_single_frame", "wk_device_cmvn",
            "wk_check_device_errors", "wk_ctc_frame_argmax", "wk_record_front", "wk_quantize_frames",
-           "wk_ctc_profile", "wk_ctc_stage_times")
+           "wk_ctc_profile", "wk_ctc_stage_times", "wk_ctc_transcribe")
 
 
 class WkConfig(C.Structure):
@@ -86,6 +86,7 @@ def _declare(L):
     L.wk_ctc_destroy.argtypes = [vp]
     L.wk_ctc_features.argtypes = [vp, vp, i64, i32, i32, i64, vp, vp]
     L.wk_ctc_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp]
+    L.wk_ctc_transcribe.argtypes = [vp, vp, i64, i32, i32, i64, vp, vp, vp]
     L.wk_ctc_frame_argmax.argtypes = [vp, i64, i32, vp, vp]
     L.wk_record_front.argtypes = [vp, i64, vp, vp, vp]
     L.wk_quantize_frames.argtypes = [vp, i64, vp, vp]
@@ -100,7 +101,7 @@ def _declare(L):
                  "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push", "wk_ctc_create",
                  "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward", "wk_wav_read", "wk_wav_load_batch",
                  "wk_augment", "wk_device_cmvn", "wk_ctc_frame_argmax", "wk_record_front",
-                 "wk_quantize_frames", "wk_ctc_profile", "wk_ctc_stage_times"):
+                 "wk_quantize_frames", "wk_ctc_profile", "wk_ctc_stage_times", "wk_ctc_transcribe"):
         getattr(L, name).restype = i32
 
 

@@ -154,6 +154,22 @@ class CTCModel:
                                    C.c_void_p(ln.data_ptr()), self._stream(torch)), "wk_ctc_forward")
         return tok, ln, lp
 
+    def decode_audio(self, audio, n_samples: int = MAX_AUDIO_SAMPLES):
+        """(B, L) float waveform -> (tokens (B, T) int32, lengths (B,) int32) on
+        device, stream-ordered: wk_ctc_transcribe, i.e. features() then
+        decode() in one call (fp16 mode: the z-score folded into the encoder)."""
+        import torch
+        x = torch.as_tensor(audio, dtype=torch.float32).to(f"cuda:{self.device}").contiguous()
+        if x.dim() == 1:
+            x = x.unsqueeze(0)
+        B, L = x.shape
+        T = 1 + n_samples // 160
+        tok = torch.empty((B, T), dtype=torch.int32, device=x.device)
+        ln = torch.empty((B,), dtype=torch.int32, device=x.device)
+        check(lib().wk_ctc_transcribe(self._h, C.c_void_p(x.data_ptr()), B, L, n_samples, L, C.c_void_p(tok.data_ptr()),
+                                      C.c_void_p(ln.data_ptr()), self._stream(torch)), "wk_ctc_transcribe")
+        return tok, ln
+
     def frame_argmax(self, batch: int, T: int):
         """decode_predictions' per-frame `predictions` (ctc.py:454) of the last
         decode/forward on this model: (batch, T) int32 on device."""
@@ -172,7 +188,10 @@ class CTCModel:
         return (seqs, lp) if return_log_probs else seqs
 
     def transcribe(self, audio, n_samples: int = MAX_AUDIO_SAMPLES) -> List[List[int]]:
-        return self.forward(self.features(audio, n_samples))
+        """audio -> token id lists (extract_features + model + decode_predictions)."""
+        tok, ln = self.decode_audio(audio, n_samples)
+        tok, ln = tok.cpu().numpy(), ln.cpu().numpy()
+        return [tok[b, :ln[b]].tolist() for b in range(tok.shape[0])]
 
     def _char_map(self, idx_to_char):
         m = idx_to_char if idx_to_char is not None else self.idx_to_char

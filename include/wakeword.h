@@ -228,6 +228,20 @@ wk_status wk_ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_
 wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T, float* d_log_probs_or_null,
                          int32_t* d_tokens, int32_t* d_lengths, void* stream);
 
+/* X1 + X2 + X3 in one call (audio -> greedy tokens): the same result as
+ * wk_ctc_features into a handle-owned buffer followed by wk_ctc_forward
+ * without log-probs (ctc.py:82-107 then :148-152, :453-471).  In fp16 mode
+ * (precision 1) with T >= 6 the z-score is not applied in place: the log-mel
+ * kernel also leaves per-pass sums, a small kernel turns them into each
+ * utterance's mean and 1/std, and the encoder applies them as it loads the
+ * raw rows -- one read and one write of the [batch][T][80] features fewer.
+ * The statistics then differ from wk_ctc_features' by float rounding, so a
+ * token may differ only where two logits are within that noise.  An
+ * utterance whose log-mel values are all equal (digital silence) is left
+ * un-normalised (std = 0 exactly).  Workspace grows on first use. */
+wk_status wk_ctc_transcribe(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n_valid, int32_t n_samples,
+                            int64_t stride, int32_t* d_tokens, int32_t* d_lengths, void* stream);
+
 /* Stage timing for measurement (bench_ctc.py): while enabled, every stage of
  * wk_ctc_features / wk_ctc_forward is bracketed by a pair of HIP events on the
  * call's stream; wk_ctc_stage_times synchronises on them and returns, per
@@ -235,7 +249,7 @@ wk_status wk_ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t
  * last wk_ctc_profile call (which clears them).  Off by default (no events). */
 enum {
   WK_CTC_STAGE_LOGMEL = 0,  /* X1 log-mel (framing, FFT, power, mel, ln)            */
-  WK_CTC_STAGE_ZSCORE,      /* X1 global z-score                                    */
+  WK_CTC_STAGE_ZSCORE,      /* X1 global z-score (wk_ctc_transcribe fp16: its statistics only) */
   WK_CTC_STAGE_ENCODER,     /* Linear 80->128 + LayerNorm + ReLU                    */
   WK_CTC_STAGE_PROJ0,       /* GRU layer 0 input projection (x W_ih^T, both dirs)   */
   WK_CTC_STAGE_GRU0,        /* GRU layer 0 recurrence (both directions)             */

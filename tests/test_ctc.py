@@ -215,6 +215,43 @@ def test_ctc_long_utterance_and_device_decode(ctc, precision):
     assert seqs == g.forward(feats)   # the argmax-only kernel agrees with the log-prob path
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_ctc_transcribe_one_call(ctc, precision):
+    """wk_ctc_transcribe (audio -> tokens in one call) against the two calls
+    it stands for.  fp32, and fp16 with T < 6: the same kernels, identical
+    tokens.  fp16 with T >= 6 folds the z-score into the encoder (statistics
+    from the log-mel passes): the oracle's argmax on every confident frame,
+    for a batch whose log-mel passes straddle utterances (T = 301 = 1 mod 6)
+    and which holds a silent utterance (std 0: left un-normalised)."""
+    import wakeword
+    m, _ = ctc
+    g = wakeword.CTCModel(CO.flat_weights(m), V, precision=precision)
+    x = O.synth_clips(23, 0, 7, 48000)
+    x[3] = 0.0
+    tok, ln = g.decode_audio(x, n_samples=48000)
+    pred = g.frame_argmax(7, 301).cpu()
+    assert int(ln.min()) >= 0 and int(ln.max()) <= 301
+    t2, l2, _ = g.decode(g.features(x, n_samples=48000))
+    pred2 = g.frame_argmax(7, 301).cpu()
+    if precision == "fp32":
+        assert torch.equal(tok, t2) and torch.equal(ln, l2)
+    else:
+        feats = CO.features(torch.from_numpy(np.delete(x, 3, axis=0)))
+        with torch.no_grad():
+            ref_lp = m(feats)
+        top2 = torch.topk(ref_lp, 2, dim=-1).values
+        ok = (top2[..., 0] - top2[..., 1]) > 0.2
+        live = [0, 1, 2, 4, 5, 6]
+        assert (pred[live] == ref_lp.argmax(-1))[ok].all()
+        assert (pred[live] == pred2[live])[ok].all()
+    # T = 4 (< 6): the unfused sequence in both modes
+    xs = O.synth_clips(29, 0, 9, 480)
+    tok, ln = g.decode_audio(xs, n_samples=480)
+    t2, l2, _ = g.decode(g.features(xs, n_samples=480))
+    assert torch.equal(tok, t2) and torch.equal(ln, l2)
+
+
 def test_ctc_state_dict_bound_by_name():
     """CTCModel binds a GRU_CTC_Model state dict by key (ctc.py:119-146), in any
     order; missing, unexpected or mis-shaped keys are rejected (host-only)."""

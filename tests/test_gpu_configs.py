@@ -162,3 +162,12 @@ def test_config5_ctc_full_batch():
         if bool(ok[j].all()):
             b = int(idx[j])
             assert tok_np[b, :ln_np[b]].tolist() == ref_seqs[j]
+    # the one-call path bench_ctc.py times (wk_ctc_transcribe: z-score folded
+    # into the encoder): the oracle's argmax on every confident frame, and the
+    # two-call path's frame decisions except at float-rounding near-ties
+    tok3, ln3 = g.decode_audio(audio, n_samples=n)
+    pred3 = g.frame_argmax(B, T).cpu()
+    assert (pred3[idx] == ref_lp.argmax(-1))[ok].all()
+    agree = float((pred3.numpy() == p).mean())
+    assert agree > 0.999, agree
+    assert int(ln3.min()) >= 0 and int(ln3.max()) <= T

@@ -8,7 +8,7 @@ recurrence, the projection GEMM) give both layers' stages their mean.
 import json
 import sys
 
-MAP = [("ctc_logmel_fft", ["logmel"]), ("ctc_zscore_kernel", ["zscore"]),
+MAP = [("ctc_logmel_fft", ["logmel"]), ("ctc_zscore_kernel", ["zscore"]), ("ctc_zstats_kernel", ["zscore"]),
        ("ctc_encoder16_kernel", ["encoder"]), ("ctc_encoder_kernel", ["encoder"]),
        ("ctc_proj16_kernel", ["proj0", "proj1"]), ("Cijk", ["proj0", "proj1"]),
        ("ctc_gru16x_kernelILi128", ["gru0"]), ("ctc_gru16x_kernelILi256", ["gru1"]),
