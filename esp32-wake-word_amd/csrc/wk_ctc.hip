@@ -1896,6 +1896,13 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       }
 #endif
       const int v = tile * kOutBN + 16 * cf + li;
+#ifdef WK_OUT_ABL_EPI   // timing ablation only (wrong tokens): one max per column block instead of the argmax epilogue
+      if (true) {   // (the empty asm keeps every accumulator, hence every MFMA, alive at no cost)
+#pragma unroll
+        for (int rf = 0; rf < kOutRF; ++rf) asm volatile("" ::"v"(acc[rf][cf]));
+        continue;
+      }
+#endif
       if (KEYED) {
         const unsigned tag = 255u - (unsigned)(4 * tile + cf);
         if (LOGITS) {

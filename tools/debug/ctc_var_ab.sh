@@ -11,6 +11,7 @@ mkdir -p gpurun_out/ab
 libof() { case "$1" in prod|env_*) echo "$R/esp32-wake-word_amd/wakeword/libwakeword.so";; *) echo "$R/variants/var_$1/libwakeword.so";; esac; }
 envof() { case "$1" in env_*) echo "${1#env_}";; *) echo "WK_AB_NONE=1";; esac; }
 for v in prod "$@"; do
+  case "$v" in abl_*) echo "$v: ablation (wrong results by design), tests skipped"; continue;; esac
   K="fp16 or config5"; [ $v = prod ] && K="ctc or config"   # the in-tree library gets every CTC test
   env $(envof $v) WAKEWORD_LIB=$(libof $v) timeout -k 10 200 python -u -m pytest tests/test_ctc.py tests/test_gpu_configs.py -m gpu -x -q \
     -k "$K" --timeout 120 --timeout-method thread > gpurun_out/ab/tests_$v.log 2>&1
