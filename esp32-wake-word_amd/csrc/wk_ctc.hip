@@ -1714,6 +1714,9 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef WK_OUT_BPIPE
 #define WK_OUT_BPIPE 0
 #endif
+#ifndef WK_OUT_EARLYDMA
+#define WK_OUT_EARLYDMA 0
+#endif
 #ifndef WK_OUT_AGPR
 #define WK_OUT_AGPR 0
 #endif
@@ -1771,7 +1774,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
                                                                           int V, __half* __restrict__ logits,
                                                                           int* __restrict__ best) {
   constexpr int kOutRF = out_rf(LOGITS), kOutRows = out_rows(LOGITS);
-  __shared__ __attribute__((aligned(16))) _Float16 bt[2][kOutBN * kOutPitch];
+  __shared__ __attribute__((aligned(1024))) _Float16 bt[2][kOutBN * kOutPitch];   // (EARLYDMA: row addresses XOR the chunk)
   // the tile's bias, staged with its W rows (an L2 load per column in the
   // epilogue stalled it); replicated x4 so one ds_read_b128 is an MFMA C operand
   __shared__ f32x4 bsh[2][kOutBN];
@@ -1826,6 +1829,24 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #pragma unroll
     for (int i = 0; i < kDmaPer; ++i) dma_piece(nt, i);
   };
+#if WK_OUT_EARLYDMA
+  // (EARLYDMA) every wave issues 4 of the tile's 32 LDS-DMA pieces right after
+  // the barrier that freed the target buffer, a whole tile ahead of its use
+  constexpr int kDmaPerAll = kOutBN * kOutK * 2 / 1024 / kOutWaves;
+  int dma_off_all[kDmaPerAll];
+#pragma unroll
+  for (int i = 0; i < kDmaPerAll; ++i) {
+    const int q = wvu * kDmaPerAll + i, rr = 2 * q + (lane >> 5), c = (lane & 31) ^ (rr & 15);
+    dma_off_all[i] = rr * (kOutK * 2) + 16 * c;
+  }
+  auto dma_all = [&](int nt) {
+#pragma unroll
+    for (int i = 0; i < kDmaPerAll; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs,
+                                               (__attribute__((address_space(3))) void*)&bt[nt & 1][(wvu * kDmaPerAll + i) * 512],
+                                               16, dma_off_all[i], nt * (kOutBN * kOutK * 2), 0, 0);
+  };
+#endif
   auto fetch = [&](int nt) {   // the tile's bias (W comes by dma_w)
     if (wave0) pb = buf_load(brs, 4 * (nt * kOutBN + tid), 0);
   };
@@ -1854,7 +1875,10 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #endif
   fetch(0);
   stash(0);
-#if WK_OUT_DMA
+#if WK_OUT_EARLYDMA
+  dma_all(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#elif WK_OUT_DMA
   dma_w(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -1953,6 +1977,79 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   wk::WkStamps _st;
   _st.init();
 #endif
+#if WK_OUT_EARLYDMA
+  // B fragments and the bias C operands by inline-asm ds_read_b128 (the
+  // compiler would make any LDS read it sees wait for the LDS-DMA in flight):
+  // row 16 cf + li, chunk (4 st + lg) ^ li = 4 st ^ (lg ^ li), so with the
+  // buffer 512-byte aligned the lane's address for step st is P ^ 64 st, and
+  // the column tiles cf are immediate offsets of 16 rows (8 KB).
+  const unsigned lds_bt = (unsigned)(uintptr_t)(__attribute__((address_space(3))) _Float16*)&bt[0][0];
+  const unsigned lds_bs = (unsigned)(uintptr_t)(__attribute__((address_space(3))) f32x4*)&bsh[0][0];
+  const unsigned P0 = lds_bt + li * (kOutPitch * 2) + 16 * (lg ^ li);
+  for (int nt = 0; nt < NT; ++nt) {
+    if (nt + 1 < NT) {
+      fetch(nt + 1);
+      dma_all(nt + 1);
+    }
+    if (lag && nt > 0) epilogue(nt - 1);
+    OUT_HIT(0);
+    const unsigned pnt = P0 + (nt & 1) * (kOutBN * kOutPitch * 2), bnt = lds_bs + (nt & 1) * (kOutBN * 16) + 16 * li;
+    // step 0's fragments and the bias, waited for; then each step issues the
+    // next step's four reads before its own 12 MFMAs and waits after them
+    h8 bfc[4], bfn[4];
+    f32x4 c[4];
+    asm volatile(
+        "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:8192\n\t"
+        "ds_read_b128 %2, %8 offset:16384\n\tds_read_b128 %3, %8 offset:24576\n\t"
+        "ds_read_b128 %4, %9\n\tds_read_b128 %5, %9 offset:256\n\t"
+        "ds_read_b128 %6, %9 offset:512\n\tds_read_b128 %7, %9 offset:768\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(bfc[0]), "=&v"(bfc[1]), "=&v"(bfc[2]), "=&v"(bfc[3]), "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3])
+        : "v"(pnt), "v"(bnt)
+        : "memory");
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      if (st + 1 < 8) {
+        const unsigned ad = pnt ^ (64u * (st + 1));
+        asm volatile(
+            "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:8192\n\t"
+            "ds_read_b128 %2, %4 offset:16384\n\tds_read_b128 %3, %4 offset:24576"
+            : "=&v"(bfn[0]), "=&v"(bfn[1]), "=&v"(bfn[2]), "=&v"(bfn[3])
+            : "v"(ad)
+            : "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (st == 0) {
+#pragma unroll
+        for (int cf = 0; cf < 4; ++cf)
+#pragma unroll
+          for (int rf = 0; rf < kOutRF; ++rf)
+            acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][0], bfc[cf], c[cf], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int rf = 0; rf < kOutRF; ++rf)
+#pragma unroll
+          for (int cf = 0; cf < 4; ++cf)
+            acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bfc[cf], acc[rf][cf], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 1 < 8) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bfn[0]), "+v"(bfn[1]), "+v"(bfn[2]), "+v"(bfn[3])::"memory");
+#pragma unroll
+        for (int cf = 0; cf < 4; ++cf) bfc[cf] = bfn[cf];
+      }
+    }
+    OUT_HIT(1);
+    if (!lag && nt + 1 < NT) stash((nt + 1) & 1);
+    OUT_HIT(2);
+    if (!lag) epilogue(nt);
+    OUT_HIT(3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this tile's LDS-DMA (issued at its start) done
+    OUT_HIT(4);
+    __syncthreads();
+    OUT_HIT(5);
+  }
+#else
   for (int nt = 0; nt < NT; ++nt) {
     if (nt + 1 < NT) fetch(nt + 1);
     const _Float16* b = bt[nt & 1];
@@ -2022,6 +2119,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     __syncthreads();
     OUT_HIT(5);
   }
+#endif
 #ifdef WK_OUT_STAMPS
   if (lane == 0 && blockIdx.x == 0 && !LOGITS)
     for (int k = 0; k < 16; ++k) atomicAdd(&g_out_stamps[wv][k], _st.st[k]);
