@@ -195,7 +195,9 @@ wk_status wk_quantize_frames(const float* d_mfcc, int64_t n_values, int8_t* d_ou
  * greedy decode (ctc.py:453-471).  The reference builds V from its corpus at
  * run time (ctc.py:261-278); here V is a parameter.  This build implements the
  * reference Config (ctc.py:21-40): hidden 128, 2 bidirectional GRU layers,
- * 80 mels, n_fft 400, hop 160. */
+ * 80 mels, n_fft 400, hop 160.  A wk_ctc handle owns its activations
+ * workspace: issue one handle's calls on one stream (or order them across
+ * streams yourself); use one handle per stream for concurrent batches. */
 typedef struct {
   int32_t vocab;    /* V, including <blank> = 0 and <unk> = 1                */
   int32_t hidden;   /* 128 */
