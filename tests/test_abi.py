@@ -63,6 +63,10 @@ def test_bad_arguments_rejected_without_gpu(L):
     assert not L.extract_mfcc(buf, 100, 16000, 320, 256, 512, 40, 13)
     cfg = _lib.WkConfig(7, 0, 0, 0, 1)   # bad mode
     assert L.wk_create(C.byref(cfg), None, C.byref(h)) == 1
+    # CTC entry points: a NULL handle is rejected before any device work
+    assert L.wk_ctc_features(None, None, 1, 48000, 48000, 48000, None, None) == 1
+    assert L.wk_ctc_forward(None, None, 1, 301, None, None, None, None) == 1
+    assert L.wk_ctc_transcribe(None, None, 1, 48000, 48000, 48000, None, None, None) == 1
 
 
 def test_analyze_mfcc_range_output(L, capfd):
