@@ -252,6 +252,28 @@ def test_ctc_transcribe_one_call(ctc, precision):
     assert torch.equal(tok, t2) and torch.equal(ln, l2)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_samples", [800, 960, 1920, 8000])
+def test_ctc_transcribe_short_utterances(ctc, n_samples):
+    """The folded z-score at small T (6, 7, 13, 51 frames): log-mel passes of
+    6 rows start mid-utterance and straddle two utterances in every pattern;
+    the fp16 one-call path must give the oracle's argmax on confident frames
+    for all 11 utterances."""
+    import wakeword
+    m, _ = ctc
+    g = wakeword.CTCModel(CO.flat_weights(m), V, precision="fp16")
+    B, T = 11, 1 + n_samples // 160
+    x = O.synth_clips(31, 0, B, n_samples)
+    tok, ln = g.decode_audio(x, n_samples=n_samples)
+    pred = g.frame_argmax(B, T).cpu()
+    with torch.no_grad():
+        ref_lp = m(CO.features(torch.from_numpy(x)))
+    top2 = torch.topk(ref_lp, 2, dim=-1).values
+    ok = (top2[..., 0] - top2[..., 1]) > 0.2
+    assert (pred == ref_lp.argmax(-1))[ok].all()
+    assert int(ln.min()) >= 0 and int(ln.max()) <= T
+
+
 def test_ctc_state_dict_bound_by_name():
     """CTCModel binds a GRU_CTC_Model state dict by key (ctc.py:119-146), in any
     order; missing, unexpected or mis-shaped keys are rejected (host-only)."""
