@@ -17,6 +17,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--cpu-clips", type=int, default=4096,
+                    help="clips in the mode-A CPU baseline sample (0: skip)")
     args = ap.parse_args()
     import torch
     import wakeword
@@ -53,6 +55,27 @@ def main():
         m = wakeword.load_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"), precision=prec)
         out[f"wk_cnn_{prec}"] = timed(lambda: _lib.check(L.wk_cnn(
             m._h.h, C.c_void_p(feats.data_ptr()), B, C.c_void_p(logits.data_ptr()), sp), "wk_cnn"))
+    if args.cpu_clips > 0:
+        # the mode-A front-end (mfcc.c) on the host, single-threaded
+        # and on the host's cores, beside wk_mfcc mode A: the C restatement
+        # (oracle/esp_mfcc_oracle.c, float radix-2 FFT path) on the same clips
+        import time
+        from oracle import build_oracle as EO
+        xs = x[:args.cpu_clips].cpu().numpy()
+        cores = min(16, len(os.sched_getaffinity(0)))
+        res = {}
+        for nt, n in ((1, max(1, args.cpu_clips // 8)), (cores, args.cpu_clips)):
+            EO.esp_mfcc_batch(xs[:min(n, 64)], n_threads=nt)
+            t0 = time.perf_counter()
+            EO.esp_mfcc_batch(xs[:n], n_threads=nt)
+            res[f"threads_{nt}"] = round(n / (time.perf_counter() - t0), 1)
+        gpu = out["wk_mfcc_mode_a"]["windows_per_s"]
+        out["cpu_baseline_mode_a"] = {
+            "value": res[f"threads_{cores}"], "unit": "windows/s", "cores": cores, "kind": "port",
+            "single_thread": res["threads_1"], "gpu_over_cpu": round(gpu / res[f"threads_{cores}"], 1),
+            "sample": f"{args.cpu_clips} clips ({max(1, args.cpu_clips // 8)} single-threaded) of the device "
+                      "generator, mfcc.c restated in C with a float radix-2 FFT (oracle/esp_mfcc_oracle.c, "
+                      "esp_mfcc_oracle_batch), gcc -O2, pthreads"}
     print(json.dumps(out))
 
 

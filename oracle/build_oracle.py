@@ -14,7 +14,7 @@ OUT = os.path.join(HERE, "_build", "libesp_mfcc_oracle.so")
 def build(force: bool = False) -> str:
     if force or not os.path.exists(OUT) or os.path.getmtime(OUT) < os.path.getmtime(SRC):
         os.makedirs(os.path.dirname(OUT), exist_ok=True)
-        subprocess.check_call(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", SRC, "-o", OUT, "-lm"])
+        subprocess.check_call(["gcc", "-O2", "-std=gnu99", "-fPIC", "-shared", "-pthread", SRC, "-o", OUT, "-lm"])
     return OUT
 
 
@@ -34,6 +34,9 @@ def lib():
         _lib.esp_mfcc_oracle_ex.restype = C.c_int
         _lib.esp_mfcc_oracle_fbank.argtypes = [C.c_int, C.c_int, C.c_int, fp]
         _lib.esp_mfcc_oracle_fbank.restype = C.c_int
+        _lib.esp_mfcc_oracle_batch.argtypes = [fp, C.c_longlong, C.c_int, C.c_longlong, C.c_int, C.c_int, C.c_int,
+                                               C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_int, fp]
+        _lib.esp_mfcc_oracle_batch.restype = C.c_int
     return _lib
 
 
@@ -49,6 +52,22 @@ def esp_mfcc(x, esp_pack: bool = True, sr: int = 16000, frame: int = 320, hop: i
     if rc < 0:
         raise ValueError("esp_mfcc_oracle rejected the arguments")
     return out[:rc]
+
+
+def esp_mfcc_batch(x, esp_pack: bool = True, n_threads: int = 1, sr: int = 16000, frame: int = 320, hop: int = 256,
+                   n_fft: int = 512, n_filters: int = 40, n_mfcc: int = 13, pre: float = 0.97) -> np.ndarray:
+    """Mode-A MFCC of (B, L) signals through the FFT path on n_threads host
+    threads -> (B, n_frames, n_mfcc) float32 (the timed CPU baseline)."""
+    x = np.ascontiguousarray(x, np.float32)
+    B, L = x.shape
+    nf = (L - frame) // hop + 1
+    out = np.zeros((B, nf, n_mfcc), np.float32)
+    fp = C.POINTER(C.c_float)
+    rc = lib().esp_mfcc_oracle_batch(x.ctypes.data_as(fp), B, L, L, sr, frame, hop, n_fft, n_filters, n_mfcc,
+                                     int(esp_pack), pre, n_threads, out.ctypes.data_as(fp))
+    if rc < 0:
+        raise ValueError("esp_mfcc_oracle_batch rejected the arguments")
+    return out
 
 
 def fbank(sr: int = 16000, n_filters: int = 40, n_fft: int = 512) -> np.ndarray:
