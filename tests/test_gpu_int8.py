@@ -33,3 +33,13 @@ def test_int8_bit_exact_vs_oracle(m8, xiaoa_sd):
     np.testing.assert_array_equal(got, want.astype(np.float32))
     det = m8.detect(x).reshape(-1).cpu().numpy()                    # audio -> fp32 front-end -> int8 CNN
     np.testing.assert_array_equal(det, got)
+
+
+def test_int8_mfma_bit_exact_at_scale(m8, xiaoa_sd):
+    """The int8 matrix-core kernel (one wave per clip, grid-stride) over 4,100
+    clips of wide-range features (input saturation, every requantisation
+    clamp): bit for bit the oracle's integer network."""
+    feats = (4.0 * np.random.default_rng(5).standard_normal((4100, 13, 63))).astype(np.float32)
+    got = m8(feats).reshape(-1).cpu().numpy()
+    want = O.kws_forward_int8(O.quantize_input(feats), O.quantize_int8(xiaoa_sd)) * 0.125
+    np.testing.assert_array_equal(got, want.astype(np.float32))
