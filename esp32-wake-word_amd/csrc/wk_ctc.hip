@@ -278,6 +278,9 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
 // LDS pitches (see the per-access notes) keep the stage-1 writes, stage-2
 // reads and pair-power writes free of bank conflicts.
 // ---------------------------------------------------------------------------
+#ifndef WK_LM_NOREAD2
+#define WK_LM_NOREAD2 1
+#endif
 #ifndef WK_LM_REGTW
 #define WK_LM_REGTW 0   // (measured 0.59 vs 0.48 ms: 2 waves per SIMD lose more than the LDS reads save) 1: window and twiddles of the lane in registers, 8 waves per workgroup (2 per SIMD)
 #endif
@@ -462,18 +465,25 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
       const f2* p2 = PW + ws2;
       f2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f}, a2 = {0.0f, 0.0f};
       f2 c0 = {0.0f, 0.0f}, c1 = {0.0f, 0.0f}, c2 = {0.0f, 0.0f};
+#if WK_LM_NOREAD2   // (A/B) single 8-byte reads: the compiler would pair them into ds_read2_b64
+      typedef const volatile __attribute__((address_space(3))) f2 vf2;
+#define LM_RD(p, i) (*(vf2*)((p) + (i)))
+#else
+#define LM_RD(p, i) ((p)[i])
+#endif
 #pragma unroll
       for (int j = 0; j < kMelW1; ++j) {
-        a0 = fma2(p1[j], f2{mw1[j], mw1[j]}, a0);
-        a1 = fma2(p1[kP2Pitch + j], f2{mw1[j], mw1[j]}, a1);
-        a2 = fma2(p1[2 * kP2Pitch + j], f2{mw1[j], mw1[j]}, a2);
+        a0 = fma2(LM_RD(p1, j), f2{mw1[j], mw1[j]}, a0);
+        a1 = fma2(LM_RD(p1, kP2Pitch + j), f2{mw1[j], mw1[j]}, a1);
+        a2 = fma2(LM_RD(p1, 2 * kP2Pitch + j), f2{mw1[j], mw1[j]}, a2);
       }
 #pragma unroll
       for (int j = 0; j < kMelW2; ++j) {
-        c0 = fma2(p2[j], f2{mw2[j], mw2[j]}, c0);
-        c1 = fma2(p2[kP2Pitch + j], f2{mw2[j], mw2[j]}, c1);
-        c2 = fma2(p2[2 * kP2Pitch + j], f2{mw2[j], mw2[j]}, c2);
+        c0 = fma2(LM_RD(p2, j), f2{mw2[j], mw2[j]}, c0);
+        c1 = fma2(LM_RD(p2, kP2Pitch + j), f2{mw2[j], mw2[j]}, c1);
+        c2 = fma2(LM_RD(p2, 2 * kP2Pitch + j), f2{mw2[j], mw2[j]}, c2);
       }
+#undef LM_RD
       float cv[6] = {c0.x, c0.y, c1.x, c1.y, c2.x, c2.y};
 #pragma unroll
       for (int f = 0; f < 6; ++f)   // + the other half (lane ^ 1)
