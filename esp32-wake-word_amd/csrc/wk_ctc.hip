@@ -278,6 +278,9 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
 // LDS pitches (see the per-access notes) keep the stage-1 writes, stage-2
 // reads and pair-power writes free of bank conflicts.
 // ---------------------------------------------------------------------------
+#ifndef WK_LM_NOPAIR
+#define WK_LM_NOPAIR 1
+#endif
 #ifndef WK_LM_NOREAD2
 #define WK_LM_NOREAD2 1
 #endif
@@ -341,6 +344,14 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     }
   }
   f2* A = L.w[wv];
+#if WK_LM_NOPAIR   // (A/B) every 8-byte LDS access single: the compiler pairs neighbours into ds_read2/write2_b64
+  typedef volatile __attribute__((address_space(3))) f2 vlf2;
+#define LM_R(p, i) (*(const vlf2*)((p) + (i)))
+#define LM_W(p, i, val) (*(vlf2*)((p) + (i)) = (val))
+#else
+#define LM_R(p, i) ((p)[i])
+#define LM_W(p, i, val) ((p)[i] = (val))
+#endif
   constexpr int kRowsPerPass = 2 * kF2Pairs;
   const int64_t passes = (rows + kRowsPerPass - 1) / kRowsPerPass;
   const int64_t pstep = (int64_t)gridDim.x * kF2Waves;
@@ -408,14 +419,14 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     // 50 i mod 64 over 32 lanes is 2 x (25 i mod 32), all distinct
     if (lact) {
 #pragma unroll
-      for (int k1 = 0; k1 < 20; ++k1) A[(g * 20 + q) * kA2Pitch + k1] = v[k1];
+      for (int k1 = 0; k1 < 20; ++k1) LM_W(A, (g * 20 + q) * kA2Pitch + k1, v[k1]);
     }
     wave_lds_sync();
     // stage 2: lane (g, k1 = q) gathers column k1: lane groups g start at
     // 40 g x 25 = 40 g mod 64 dwords, so half-waves touch disjoint banks
     if (lact) {
 #pragma unroll
-      for (int n2 = 0; n2 < 20; ++n2) v[n2] = cmul2(A[(g * 20 + n2) * kA2Pitch + q], WK_LM_REGTW ? twreg[n2] : L.tw[q][n2]);
+      for (int n2 = 0; n2 < 20; ++n2) v[n2] = cmul2(LM_R(A, (g * 20 + n2) * kA2Pitch + q), WK_LM_REGTW ? twreg[n2] : L.tw[q][n2]);
     }
     dft20(v);   // Z[q + 20 k2] in v[k2]
     // exchange (the A reads of this wave are done: one wave's LDS ops complete in order)
@@ -423,7 +434,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     if (lact) {
       f2* e = E + (g * 20 + q) * kE2Pitch;
 #pragma unroll
-      for (int j = 0; j < 10; ++j) e[j] = v[10 + j];
+      for (int j = 0; j < 10; ++j) LM_W(e, j, v[10 + j]);
       if (q == 0) e[10] = v[0];
     }
     wave_lds_sync();
@@ -434,7 +445,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     {
       const f2* base = E + (g * 20 + (q == 0 ? 0 : 20 - q)) * kE2Pitch + (q == 0 ? 1 : 0);
 #pragma unroll
-      for (int k2 = 0; k2 < 10; ++k2) pp[k2] = base[9 - k2];
+      for (int k2 = 0; k2 < 10; ++k2) pp[k2] = LM_R(base, 9 - k2);
     }
     wave_lds_sync();
     // pair powers {|Z + conj Z'|^2, |Z - conj Z'|^2} = 4 {P_a, P_b}; row pitch
@@ -446,7 +457,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
       for (int k2 = 0; k2 < 10; ++k2) {
         const f2 sa = f2{v[k2].x + pp[k2].x, v[k2].y - pp[k2].y};   // Z + conj Z'
         const f2 sb = f2{v[k2].x - pp[k2].x, v[k2].y + pp[k2].y};   // Z - conj Z'
-        pr[20 * k2] = f2{__builtin_fmaf(sa.x, sa.x, sa.y * sa.y), __builtin_fmaf(sb.x, sb.x, sb.y * sb.y)};
+        LM_W(pr, 20 * k2, (f2{__builtin_fmaf(sa.x, sa.x, sa.y * sa.y), __builtin_fmaf(sb.x, sb.x, sb.y * sb.y)}));
       }
       if (q == 0) {   // bin 200 is its own partner: 4 {Re^2, Im^2}
         const f2 z = v[10];
