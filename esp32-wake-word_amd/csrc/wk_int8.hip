@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void wk_int8_cnn_kernel(const float* __restric
 // 4 lg .. 4 lg + 3.  (Any K order the hardware uses applies to A and B alike.)
 // ---------------------------------------------------------------------------
 typedef int i32x4 __attribute__((ext_vector_type(4)));
-constexpr int kQW = 4;                        // waves per block
+constexpr int kQW = 8;                        // waves per block (2 per SIMD)
 constexpr int kX0 = 66 * 16, kA1 = 34 * 32, kA2 = 18 * 64;   // per-wave images: [t][ci] int8, zero guards
 
 __device__ __forceinline__ int q_even(int v) {   // pool partner: the other lane of the pair (li ^ 1)
@@ -163,6 +163,8 @@ __global__ __launch_bounds__(64 * kQW) void wk_int8_mfma_kernel(const float* __r
                                                                  float* __restrict__ logits) {
   __shared__ int8_t w[kW0 + kW3 + kW6 + kM23 + kM24];
   __shared__ __attribute__((aligned(16))) int8_t img[kQW][kX0 + kA1 + kA2 + 128];
+  __shared__ i32x4 fimg[10][64];
+  __shared__ int m23t[32][64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   for (int i = tid; i < (int)sizeof(w); i += 64 * kQW) w[i] = wq[i];
@@ -188,22 +190,21 @@ __global__ __launch_bounds__(64 * kQW) void wk_int8_mfma_kernel(const float* __r
     return i32x4{(int)pack4(b[0], b[1], b[2], b[3]), (int)pack4(b[4], b[5], b[6], b[7]),
                  (int)pack4(b[8], b[9], b[10], b[11]), (int)pack4(b[12], b[13], b[14], b[15])};
   };
-  i32x4 f1[2], f2[4][2], f3[8][3];
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) f1[ct] = frag(W0, 13, 16, 32, ct, 0);
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-    for (int st = 0; st < 2; ++st) f2[ct][st] = frag(W3, 32, 32, 64, ct, st);
+  // conv3's 24 fragments stay in VGPRs; conv1's 2 and conv2's 8 live in a
+  // block-shared LDS image [fragment][lane] (each wave builds some of them)
+  i32x4 f3[8][3];
 #pragma unroll
   for (int ct = 0; ct < 8; ++ct)
 #pragma unroll
     for (int st = 0; st < 3; ++st) f3[ct][st] = frag(W6, 64, 64, 128, ct, st);
-  int m23[32];   // lane o: column o of M23 as 4-byte groups over c
-#pragma unroll
-  for (int j = 0; j < 32; ++j)
-    m23[j] = (int)pack4(M23[(4 * j) * 64 + lane], M23[(4 * j + 1) * 64 + lane], M23[(4 * j + 2) * 64 + lane],
-                        M23[(4 * j + 3) * 64 + lane]);
+  for (int fi = wv; fi < 10; fi += kQW)
+    fimg[fi][lane] = fi < 2 ? frag(W0, 13, 16, 32, fi, 0) : frag(W3, 32, 32, 64, (fi - 2) >> 1, (fi - 2) & 1);
+  __syncthreads();
+  // classifier.0: lane o's column of M23 as 4-byte groups over c, [group][lane] in LDS
+  for (int j = wv; j < 32; j += kQW)
+    m23t[j][lane] = (int)pack4(M23[(4 * j) * 64 + lane], M23[(4 * j + 1) * 64 + lane], M23[(4 * j + 2) * 64 + lane],
+                               M23[(4 * j + 3) * 64 + lane]);
+  __syncthreads();
   const int m24 = M24[lane];
   const int64_t wstride = (int64_t)gridDim.x * kQW;
   for (int64_t b = (int64_t)blockIdx.x * kQW + wv; b < batch; b += wstride) {
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(64 * kQW) void wk_int8_mfma_kernel(const float* __r
       if (lg < 3) bx = *reinterpret_cast<const i32x4*>(x0 + (t + lg) * 16);
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
-        const i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(f1[ct], bx, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(fimg[ct][lane], bx, i32x4{0, 0, 0, 0}, 0, 0, 0);
         int q[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -249,7 +250,8 @@ __global__ __launch_bounds__(64 * kQW) void wk_int8_mfma_kernel(const float* __r
         i32x4 bx = i32x4{0, 0, 0, 0};
         if (k < 3) bx = *reinterpret_cast<const i32x4*>(a1 + (t + k) * 32 + ci0);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f2[ct][st], bx, acc[ct], 0, 0, 0);
+        for (int ct = 0; ct < 4; ++ct)
+          acc[ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fimg[2 + 2 * ct + st][lane], bx, acc[ct], 0, 0, 0);
       }
       const int tp = t >> 1;
 #pragma unroll
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(64 * kQW) void wk_int8_mfma_kernel(const float* __r
     // MatMul 128 -> 64 (s = 10) + ReLU: lane o, 32 dot4 over the broadcast g bytes
     int acc = 0;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) acc = __builtin_amdgcn_sdot4(*reinterpret_cast<const int*>(gq + 4 * j), m23[j], acc, false);
+    for (int j = 0; j < 32; ++j) acc = __builtin_amdgcn_sdot4(*reinterpret_cast<const int*>(gq + 4 * j), m23t[j][lane], acc, false);
     const int hid = max(0, rq(acc, 10));
     int v = hid * m24;   // MatMul 64 -> 1 (s = 10)
 #pragma unroll
