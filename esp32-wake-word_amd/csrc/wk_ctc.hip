@@ -772,6 +772,9 @@ typedef _Float16 h8e __attribute__((ext_vector_type(8)));
 // Output rows are time-major (row t B + b for input row b T + t): the fp16
 // path keeps every [rows][.] tensor after the encoder in that order, so that a
 // GRU step's 16 utterances are 16 adjacent rows of the gate inputs and outputs.
+#ifndef WK_ENC_PF
+#define WK_ENC_PF 1   // fp16 encoder: 16-row blocks of input in flight per wave
+#endif
 // NORM (wk_ctc_transcribe): the input rows are raw log-mel; each is z-scored
 // with its utterance's zs = {mean, 1/std} (ctc_zstats_kernel) as it is loaded.
 template <bool NORM>
@@ -809,20 +812,21 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
   // waited for everything: ~60 % of wave-cycles were waits, PMC).
   const __amdgpu_buffer_rsrc_t irs = make_rsrc(in, (uint32_t)(rows * kMels * 4));   // < 2^31 B (host check)
   const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, (uint32_t)(rows * kH * 2));
-  float4 xr[KS][2];
-  auto load_blk = [&](int64_t blk) {
+  // WK_ENC_PF blocks of input rows in flight per wave (a block's compute is
+  // far shorter than the HBM latency)
+  float4 xr[WK_ENC_PF][KS][2];
+  auto load_blk = [&](int64_t blk, float4 (&x)[KS][2]) __attribute__((always_inline)) {
     const int64_t r = blk * 16 + li;
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
       const int k0 = 32 * st + 8 * lg;
       const int off = r < rows && k0 < kMels ? (int)(r * kMels + k0) * 4 : 0x7FFFFFE0;   // past num_records: 0
-      xr[st][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(irs, off, 0, 0));
-      xr[st][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(irs, off + 16, 0, 0));
+      x[st][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(irs, off, 0, 0));
+      x[st][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(irs, off + 16, 0, 0));
     }
   };
-  int64_t blk = (int64_t)blockIdx.x * 4 + wv;
-  load_blk(blk);
-  for (; blk < nblk; blk += (int64_t)gridDim.x * 4) {
+  const int64_t G = (int64_t)gridDim.x * 4;
+  auto body = [&](int64_t blk, float4 (&x)[KS][2]) __attribute__((always_inline)) {
     const int64_t r = blk * 16 + li;   // this lane's row
     const int rr = r < rows ? (int)r : 0;   // rows < 2^31 (host check)
     const int ub = rr / T, ut = rr - ub * T;
@@ -831,7 +835,7 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
       const float2 z = zs[ub];
 #pragma unroll
       for (int st = 0; st < KS; ++st) {
-        const float4 a = xr[st][0], b = xr[st][1];
+        const float4 a = x[st][0], b = x[st][1];
         xb[st] = h8e{(_Float16)((a.x - z.x) * z.y), (_Float16)((a.y - z.x) * z.y), (_Float16)((a.z - z.x) * z.y),
                      (_Float16)((a.w - z.x) * z.y), (_Float16)((b.x - z.x) * z.y), (_Float16)((b.y - z.x) * z.y),
                      (_Float16)((b.z - z.x) * z.y), (_Float16)((b.w - z.x) * z.y)};
@@ -839,12 +843,12 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
     } else {
 #pragma unroll
       for (int st = 0; st < KS; ++st) {
-        const float4 a = xr[st][0], b = xr[st][1];
+        const float4 a = x[st][0], b = x[st][1];
         xb[st] = h8e{(_Float16)a.x, (_Float16)a.y, (_Float16)a.z, (_Float16)a.w,
                      (_Float16)b.x, (_Float16)b.y, (_Float16)b.z, (_Float16)b.w};
       }
     }
-    load_blk(blk + (int64_t)gridDim.x * 4);   // the next block (past the end: zeros, unused)
+    load_blk(blk + WK_ENC_PF * G, x);   // the block WK_ENC_PF ahead into this slot (past the end: zeros, unused)
     f32x4 acc[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc[ct] = *reinterpret_cast<const f32x4*>(&pb[0][16 * ct + 4 * lg]);   // + bias
@@ -882,6 +886,16 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
       for (int i = 0; i < 4; ++i) y[i] = (_Float16)fmaxf(__builtin_fmaf((acc[ct][i] - mean) * rs, g[i], bt[i]), 0.0f);
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, y), ors,
                                             orow + c0 * 2, 0, 0);
+    }
+  };
+  int64_t blk = (int64_t)blockIdx.x * 4 + wv;
+#pragma unroll
+  for (int u = 0; u < WK_ENC_PF; ++u) load_blk(blk + u * G, xr[u]);
+  for (; blk < nblk; blk += WK_ENC_PF * G) {
+#pragma unroll
+    for (int u = 0; u < WK_ENC_PF; ++u) {
+      if (blk + u * G >= nblk) break;   // (wave-uniform)
+      body(blk + u * G, xr[u]);
     }
   }
 }
