@@ -772,6 +772,9 @@ typedef _Float16 h8e __attribute__((ext_vector_type(8)));
 // Output rows are time-major (row t B + b for input row b T + t): the fp16
 // path keeps every [rows][.] tensor after the encoder in that order, so that a
 // GRU step's 16 utterances are 16 adjacent rows of the gate inputs and outputs.
+#ifndef WK_GRU_HSINGLE
+#define WK_GRU_HSINGLE 0
+#endif
 #ifndef WK_ENC_PF
 #define WK_ENC_PF 1   // fp16 encoder: 16-row blocks of input in flight per wave
 #endif
@@ -1504,8 +1507,15 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
     __builtin_amdgcn_sched_barrier(0);
     GRU_HIT(1);
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 2; ++q) {
+#if WK_GRU_HSINGLE   // (A/B) two single 8-byte writes (the compiler pairs them into ds_write2st64_b64)
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      typedef volatile __attribute__((address_space(3))) u32x2 vlu2;
+      if (!(WK_GRU_LDSABL & 8)) *(vlu2*)&h16[cur ^ 1][(16 * q + n) * kGxHP + u0] = __builtin_bit_cast(u32x2, o[q]);
+#else
       if (!(WK_GRU_LDSABL & 8)) *reinterpret_cast<uint2*>(&h16[cur ^ 1][(16 * q + n) * kGxHP + u0]) = __builtin_bit_cast(uint2, o[q]);
+#endif
+    }
     cur ^= 1;
     GRU_HIT(2);
 #if WK_GRU_FLAGS
