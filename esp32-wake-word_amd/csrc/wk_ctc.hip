@@ -1765,6 +1765,13 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef WK_OUT_AGPR
 #define WK_OUT_AGPR 0
 #endif
+// RING4: four W buffers, the leading waves' LDS-DMA two tiles ahead and one
+// barrier per two tiles (the barrier and its refill were ~10 % of a tile)
+#ifndef WK_OUT_RING4
+#define WK_OUT_RING4 0
+#endif
+static_assert(!WK_OUT_RING4 || (WK_OUT_DMA && !WK_OUT_EARLYDMA), "RING4 is a form of the LDS-DMA path");
+constexpr int kOutNB = WK_OUT_RING4 ? 4 : 2, kOutAhead = WK_OUT_RING4 ? 2 : 1;
 constexpr int kOutK = 2 * kH, kOutBN = 64, kOutPitch = kOutK, kOutRF = WK_OUT_RF, kOutWaves = WK_OUT_WAVES;
 // W tile rows are 512 B with their 16-byte chunks XOR-swizzled by the row's
 // low 4 bits (chunk c of row n at c ^ (n & 15)): a ds_read_b128 B fragment
@@ -1819,10 +1826,10 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
                                                                           int V, __half* __restrict__ logits,
                                                                           int* __restrict__ best) {
   constexpr int kOutRF = out_rf(LOGITS), kOutRows = out_rows(LOGITS);
-  __shared__ __attribute__((aligned(1024))) _Float16 bt[2][kOutBN * kOutPitch];   // (EARLYDMA: row addresses XOR the chunk)
+  __shared__ __attribute__((aligned(1024))) _Float16 bt[kOutNB][kOutBN * kOutPitch];   // (EARLYDMA: row addresses XOR the chunk)
   // the tile's bias, staged with its W rows (an L2 load per column in the
   // epilogue stalled it); replicated x4 so one ds_read_b128 is an MFMA C operand
-  __shared__ f32x4 bsh[2][kOutBN];
+  __shared__ f32x4 bsh[kOutNB][kOutBN];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const bool wave0 = __builtin_amdgcn_readfirstlane(wv) == 0;
@@ -1866,7 +1873,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   }
   auto dma_piece = [&](int nt, int i) {
     const int q = wvu * kDmaPer + i;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)&bt[nt & 1][q * 512], 16,
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)&bt[nt & (kOutNB - 1)][q * 512], 16,
                                              dma_off[i], nt * (kOutBN * kOutK * 2), 0, 0);
   };
   auto dma_w = [&](int nt) {
@@ -1925,6 +1932,11 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #elif WK_OUT_DMA
   dma_w(0);
+  for (int t = 1; t < kOutAhead && t < NT; ++t) {
+    fetch(t);
+    stash(t);
+    dma_w(t);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   __syncthreads();
@@ -2096,8 +2108,8 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   }
 #else
   for (int nt = 0; nt < NT; ++nt) {
-    if (nt + 1 < NT) fetch(nt + 1);
-    const _Float16* b = bt[nt & 1];
+    if (nt + kOutAhead < NT) fetch(nt + kOutAhead);
+    const _Float16* b = bt[nt & (kOutNB - 1)];
     if (lag && nt > 0) epilogue(nt - 1);
     OUT_HIT(0);
 #if WK_OUT_BPIPE
@@ -2129,7 +2141,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       if (st == 0) {
 #pragma unroll
         for (int cf = 0; cf < 4; ++cf) {
-          const f32x4 c0 = bsh[nt & 1][16 * cf + li];
+          const f32x4 c0 = bsh[nt & (kOutNB - 1)][16 * cf + li];
 #pragma unroll
           for (int rf = 0; rf < kOutRF; ++rf)
             acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][0], bf[cf], c0, 0, 0, 0);
@@ -2147,21 +2159,27 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     }
     OUT_HIT(1);
 #if WK_OUT_DMA
-    if (!lag && nt + 1 < NT) {   // after this wave's last LDS read of the period
-      stash((nt + 1) & 1);
-      if (!WK_OUT_DMA_SPREAD) dma_w(nt + 1);
+    if (!lag && nt + kOutAhead < NT) {   // after this wave's last LDS read of the period
+      stash((nt + kOutAhead) & (kOutNB - 1));
+      if (!WK_OUT_DMA_SPREAD) dma_w(nt + kOutAhead);
     }
 #endif
     OUT_HIT(2);
     if (!lag) epilogue(nt, WK_OUT_DMA && WK_OUT_DMA_SPREAD && nt + 1 < NT && wvu < kDmaWaves ? nt + 1 : -1);
     OUT_HIT(3);
+    // (RING4) tile nt + 2 is DMA'd into the buffer tile nt - 2 used: every wave
+    // left that tile behind a barrier (after nt - 1 for even nt, after nt - 2
+    // for odd), and the barrier after each odd tile publishes the tiles the
+    // two periods before it issued
+    if (!WK_OUT_RING4 || (nt & 1)) {
 #if WK_OUT_DMA
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // LDS-DMA done (the barrier's own wait omits it)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // LDS-DMA done (the barrier's own wait omits it)
 #else
-    if (nt + 1 < NT) stash((nt + 1) & 1);
+      if (nt + 1 < NT) stash((nt + 1) & 1);
 #endif
-    OUT_HIT(4);
-    __syncthreads();
+      OUT_HIT(4);
+      __syncthreads();
+    }
     OUT_HIT(5);
   }
 #endif
