@@ -1762,9 +1762,6 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef WK_OUT_EARLYDMA
 #define WK_OUT_EARLYDMA 0
 #endif
-#ifndef WK_OUT_AGPR
-#define WK_OUT_AGPR 0
-#endif
 // RING4: four W buffers, the leading waves' LDS-DMA two tiles ahead and one
 // barrier per two tiles (the barrier and its refill were ~10 % of a tile)
 #ifndef WK_OUT_RING4
