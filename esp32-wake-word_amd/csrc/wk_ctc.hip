@@ -1769,7 +1769,12 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #endif
 static_assert(!WK_OUT_RING4 || (WK_OUT_DMA && !WK_OUT_EARLYDMA), "RING4 is a form of the LDS-DMA path");
 constexpr int kOutNB = WK_OUT_RING4 ? 4 : 2, kOutAhead = WK_OUT_RING4 ? 2 : 1;
-constexpr int kOutK = 2 * kH, kOutBN = 64, kOutPitch = kOutK, kOutRF = WK_OUT_RF, kOutWaves = WK_OUT_WAVES;
+#ifndef WK_OUT_BN
+#define WK_OUT_BN 64     // W tile columns (64; 32 and 128 measured)
+#endif
+constexpr int kOutK = 2 * kH, kOutBN = WK_OUT_BN, kOutCF = kOutBN / 16, kOutPitch = kOutK, kOutRF = WK_OUT_RF,
+              kOutWaves = WK_OUT_WAVES;
+static_assert(kOutBN == 64 || ((kOutBN == 32 || kOutBN == 128) && !WK_OUT_EARLYDMA), "W tile width");
 // W tile rows are 512 B with their 16-byte chunks XOR-swizzled by the row's
 // low 4 bits (chunk c of row n at c ^ (n & 15)): a ds_read_b128 B fragment
 // (row 16 cf + li, chunk 4 st + lg) then hits 16 distinct 4-bank windows in
@@ -1829,7 +1834,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   __shared__ f32x4 bsh[kOutNB][kOutBN];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
-  const bool wave0 = __builtin_amdgcn_readfirstlane(wv) == 0;
+  const bool wave0 = __builtin_amdgcn_readfirstlane(wv) < (kOutBN + 63) / 64;   // the waves that stage the tile's bias
   const int64_t row0 = (int64_t)blockIdx.x * kOutRows + 16 * kOutRF * wv;
   // A fragments: rows row0 + 16 rf + li, k = 32 s + 8 lg .. +7
   h8 a[kOutRF][8];
@@ -1900,7 +1905,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     if (wave0) pb = buf_load(brs, 4 * (nt * kOutBN + tid), 0);
   };
   auto stash = [&](int buf) {
-    if (wave0) bsh[buf][tid] = f32x4{pb, pb, pb, pb};
+    if (wave0 && tid < kOutBN) bsh[buf][tid] = f32x4{pb, pb, pb, pb};
   };
 #else
   uint4 pre[kOutPre];
@@ -1919,7 +1924,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
       *reinterpret_cast<uint4*>(&bt[buf][rr * kOutPitch + 8 * out_chunk(rr, ch)]) = pre[i];
     }
-    if (wave0) bsh[buf][tid] = f32x4{pb, pb, pb, pb};
+    if (wave0 && tid < kOutBN) bsh[buf][tid] = f32x4{pb, pb, pb, pb};
   };
 #endif
   fetch(0);
@@ -1957,7 +1962,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   const bool lag = WK_OUT_SKEW && ((__builtin_amdgcn_readfirstlane(wv) >> 2) & 1);
   // The bias is the MFMAs' initial C operand (one ds_read_b128 of the
   // replicated bias per column tile), so the epilogue is compare + select.
-  f32x4 acc[kOutRF][4];
+  f32x4 acc[kOutRF][kOutCF];
   // (FULL: every column of the tile is < V -- all tiles but a ragged last
   // one -- so the per-lane bound check and its exec-mask blocks go)
 #ifndef WK_OUT_DMA_SPREAD
@@ -1966,11 +1971,11 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   auto epilogue_t = [&](int tile, auto full, int dma_tile) __attribute__((always_inline)) {
     // column v = 64 tile + 16 cf + li, rows row0 + 16 rf + 4 lg + i
 #pragma unroll
-    for (int cf = 0; cf < 4; ++cf) {
+    for (int cf = 0; cf < kOutCF; ++cf) {
 #if WK_OUT_DMA
       if (dma_tile >= 0) {
 #pragma unroll
-        for (int i = cf * kDmaPer / 4; i < (cf + 1) * kDmaPer / 4; ++i) dma_piece(dma_tile, i);
+        for (int i = cf * kDmaPer / kOutCF; i < (cf + 1) * kDmaPer / kOutCF; ++i) dma_piece(dma_tile, i);
       }
 #endif
       const int v = tile * kOutBN + 16 * cf + li;
@@ -1982,7 +1987,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       }
 #endif
       if (KEYED) {
-        const unsigned tag = 255u - (unsigned)(4 * tile + cf);
+        const unsigned tag = 255u - (unsigned)(kOutCF * tile + cf);
         if (LOGITS) {
 #pragma unroll
           for (int rf = 0; rf < kOutRF; ++rf)
@@ -2113,9 +2118,9 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     // B fragments one k-step ahead: step st + 1's four reads are issued
     // before step st's MFMAs (the compiler otherwise slots them among the last
     // MFMAs of the step, ~1-4 MFMAs before their use)
-    h8 bfp[2][4];
+    h8 bfp[2][kOutCF];
 #pragma unroll
-    for (int cf = 0; cf < 4; ++cf)
+    for (int cf = 0; cf < kOutCF; ++cf)
       bfp[0][cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, lg));
 #endif
 #pragma unroll
@@ -2123,21 +2128,21 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #if WK_OUT_BPIPE
       if (st + 1 < 8) {
 #pragma unroll
-        for (int cf = 0; cf < 4; ++cf)
+        for (int cf = 0; cf < kOutCF; ++cf)
           bfp[(st + 1) & 1][cf] =
               *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, 4 * (st + 1) + lg));
       }
       __builtin_amdgcn_sched_barrier(0);   // the next step's reads stay ahead of this step's MFMAs
       const h8* bf = bfp[st & 1];
 #else
-      h8 bf[4];
+      h8 bf[kOutCF];
 #pragma unroll
-      for (int cf = 0; cf < 4; ++cf)
+      for (int cf = 0; cf < kOutCF; ++cf)
         bf[cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, 4 * st + lg));
 #endif
       if (st == 0) {
 #pragma unroll
-        for (int cf = 0; cf < 4; ++cf) {
+        for (int cf = 0; cf < kOutCF; ++cf) {
           const f32x4 c0 = bsh[nt & (kOutNB - 1)][16 * cf + li];
 #pragma unroll
           for (int rf = 0; rf < kOutRF; ++rf)
@@ -2147,7 +2152,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #pragma unroll
         for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
-          for (int cf = 0; cf < 4; ++cf)
+          for (int cf = 0; cf < kOutCF; ++cf)
             acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf[cf], acc[rf][cf], 0, 0, 0);
       }
 #if WK_OUT_BPIPE
@@ -2796,7 +2801,7 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
       // fused output layer + argmax; fp16 logits are written only for log_softmax
       const dim3 og((unsigned)((rows + out_rows(d_log_probs != nullptr) - 1) / out_rows(d_log_probs != nullptr)));
       s = timed(c, WK_CTC_STAGE_OUTPUT, st, [&]() -> wk_status {
-        const bool keyed = WK_OUT_KEYED && V <= 64 * kOutBN;   // the tag holds 4 tile + cf in 8 bits
+        const bool keyed = WK_OUT_KEYED && V <= 16 * 256;   // the tag holds kOutCF tile + cf in 8 bits
         if (d_log_probs) {
           hipLaunchKernelGGL((keyed ? ctc_out_argmax16_kernel<true, true> : ctc_out_argmax16_kernel<true, false>), og,
                              dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, c->logits16, c->best);
