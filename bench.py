@@ -143,32 +143,64 @@ def spawn_ranks(argv, n: int, timeout: float = None) -> int:
     return rc
 
 
-def cpu_baseline(seconds: float):
+def host_threads():
+    """CPU threads this process may run on: the affinity mask, capped by the
+    cgroup CPU quota when one is set (a GPU box shows the whole machine's CPUs
+    in its affinity mask but grants each GPU a share of them)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+CPU_BATCHES = (256, 4096)   # BASELINE.md section 3 / SURVEY 8(d): batch 256 and 4096
+
+
+def cpu_baseline(seconds: float, batches=CPU_BATCHES):
     """The ml_models CPU path (torch fp32 restatement, oracle/wk_torch_cpu.py) on
-    the host cores, timed on a bounded sample of the same synthetic workload."""
-    import numpy as np
+    the host cores, timed on a bounded sample of the same synthetic workload:
+    about seconds / len(batches) per batch size, all host threads
+    (torch.set_num_threads), outside any GPU timing.  `value` is the best of
+    the batch sizes; every batch size's rate is listed."""
     import torch
     from oracle import wk_oracle as O
     from oracle.wk_torch_cpu import TorchCpuPath
     from wakeword.onnx_reader import read_onnx, xiaoa_state_dict
-    inits, _, _ = read_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"))
-    path = TorchCpuPath(xiaoa_state_dict(inits))
-    batch = 256
-    x = torch.from_numpy(O.synth_clips(1234, 0, batch))
-    path(x)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        path(x)
-        n += batch
-        el = time.perf_counter() - t0
-        if el >= seconds and n >= 4 * batch:
-            break
-    return {"value": round(n / el, 1), "unit": "windows/s", "cores": torch.get_num_threads(),
-            "host_cpus": len(os.sched_getaffinity(0)),
+    threads, affinity, quota = host_threads()
+    old = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        inits, _, _ = read_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"))
+        path = TorchCpuPath(xiaoa_state_dict(inits))
+        per = {}
+        parts = []
+        for batch in batches:
+            x = torch.from_numpy(O.synth_clips(1234, 0, batch))
+            path(x)  # warm-up
+            n, t0 = 0, time.perf_counter()
+            while True:
+                path(x)
+                n += batch
+                el = time.perf_counter() - t0
+                if el >= seconds / len(batches) and n >= 2 * batch:
+                    break
+            per[str(batch)] = round(n / el, 1)
+            parts.append(f"batch {batch}: {n} windows in {el:.1f} s")
+    finally:
+        torch.set_num_threads(old)
+    best = max(per, key=per.get)
+    return {"value": per[best], "unit": "windows/s", "cores": threads, "batch": int(best),
+            "by_batch": per, "host_cpus": affinity, "cgroup_cpu_quota": quota,
             "kind": "port",
-            "sample": f"{n} windows = {n // batch} batches of {batch} synthetic clips (seed 1234), "
-                      f"{el:.1f} s; torch-CPU fp32 restatement of the torchaudio MFCC+CMVN front-end "
-                      f"+ LightweightKWS on the xiaoa.onnx weights (oracle/wk_torch_cpu.py)"}
+            "sample": "; ".join(parts) + " (synthetic clips, seed 1234); torch-CPU fp32 restatement of the "
+                      "torchaudio MFCC+CMVN front-end + LightweightKWS on the xiaoa.onnx weights "
+                      f"(oracle/wk_torch_cpu.py), torch.set_num_threads({threads})"}
 
 
 def load_traffic(precision="fp32"):
@@ -182,6 +214,32 @@ def load_traffic(precision="fp32"):
         return None, None
 
 
+def init_rank(args, env, torch, dist):
+    """This rank's (world, rank, local device, shared) from torchrun's
+    environment, with the process group formed: nccl (RCCL) with the rank's
+    own device as `device_id`, or gloo.  shared = more ranks than visible
+    GPUs (a gloo rehearsal of the N>1 path on one GPU): the line then carries
+    no throughput."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    rank = int(env.get("RANK", "0"))
+    local = int(env.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and local >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPU(s) visible")
+    shared = world > ndev
+    local = local % ndev   # (gloo rehearsal: ranks may share a GPU)
+    torch.cuda.set_device(local)
+    if world > 1:
+        env.setdefault("MASTER_ADDR", "127.0.0.1")
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
+    return world, rank, local, shared
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -193,22 +251,7 @@ def main():
     from wakeword import _lib
     from wakeword.shard import weak_shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
-    ndev = torch.cuda.device_count()
-    if args.dist_backend == "nccl" and local >= ndev:
-        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPU(s) visible")
-    local = local % ndev   # (gloo rehearsal: ranks may share a GPU)
-    torch.cuda.set_device(local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        else:
-            dist.init_process_group("gloo")
+    world, rank, local, shared = init_rank(args, os.environ, torch, dist)
 
     def barrier():
         if world > 1:
@@ -309,6 +352,15 @@ def main():
             "logits_finite": True,
             "device_errors": 0,
         }
+        if shared:
+            # ranks time-share one GPU: the launch path ran, but nothing here is
+            # an N-GPU throughput or a kernel rate
+            out["value"] = None
+            out["rehearsal"] = True
+            out["note"] = (f"{world} ranks shared {torch.cuda.device_count()} GPU(s) over {args.dist_backend}: "
+                           "rehearsal of the N>1 launch, barrier and max-over-ranks path; no throughput")
+            for k in ("achieved", "frac", "launch_ms", "hbm_gbs_algorithmic"):
+                out["roofline"][k] = None
         if traffic_src:
             out["roofline"]["traffic_source"] = traffic_src
         if world == 1 and not args.no_cpu_baseline:

@@ -272,16 +272,27 @@ static wk_status forward_impl(wk_handle* h, const void* d_audio, int32_t dtype, 
     }
     // Every exit after the first launch (a failed later launch included) marks
     // the workspace busy until this stream's queued chunks are done, so the next
-    // call on another stream still waits for them.
+    // call on another stream still waits for them.  If the event cannot be
+    // recorded, this stream is drained instead (the workspace is then idle)
+    // and the failure is reported.
     bool launched = false;
     struct WsRelease {
       wk_handle* h;
       std::unique_lock<std::mutex>& lk;
       bool& launched;
       hipStream_t st;
-      ~WsRelease() {
-        if (lk.owns_lock() && launched && hipEventRecord(h->ws_free, st) == hipSuccess) h->ws_used = true;
+      hipError_t release() {
+        if (!lk.owns_lock() || !launched) return hipSuccess;
+        launched = false;
+        hipError_t e = hipEventRecord(h->ws_free, st);
+        if (e == hipSuccess) {
+          h->ws_used = true;
+          return e;
+        }
+        if (hipStreamSynchronize(st) == hipSuccess) h->ws_used = false;   // drained: nothing left to wait for
+        return e;
       }
+      ~WsRelease() { (void)release(); }
     } ws_release{h, ws_lock, launched, (hipStream_t)stream};
     for (int64_t c0 = 0; c0 < batch; c0 += h->ws_clips) {
       const int64_t n = batch - c0 < h->ws_clips ? batch - c0 : h->ws_clips;
@@ -296,6 +307,8 @@ static wk_status forward_impl(wk_handle* h, const void* d_audio, int32_t dtype, 
                                       (hipStream_t)stream, d_err);
       if (e != hipSuccess) return hip_fail(e, "cnn launch");
     }
+    const hipError_t er = ws_release.release();
+    if (er != hipSuccess) return hip_fail(er, "hipEventRecord(workspace)");
     return WK_OK;
   });
 }
@@ -350,97 +363,62 @@ wk_status wk_device_cmvn(const void* d_frames, int32_t dtype, int64_t n_frames, 
 // ---------------------------------------------------------------------------
 // mfcc.h compatibility shims (main/esp_mfcc/mfcc.h:10-17, mfcc.c:431-563).
 // ---------------------------------------------------------------------------
+}  // extern "C"
+
 static std::mutex g_compat_mu;
 static wk_handle* g_compat = nullptr;
 
-float* extract_mfcc(const float* signal, int signal_len, int sampling_rate, int frame_size, int hop_size, int n_fft,
-                    int n_filters, int n_mfcc) {
-  // mfcc.c:434-437: NULL signal or a signal shorter than one frame -> NULL.
-  if (!signal || signal_len < frame_size || frame_size <= 0) {
-    fprintf(stderr, "E (MFCC) Invalid signal parameters\n");
-    return nullptr;
+// The fixed-geometry mode-A handle of the shims (reference configuration).
+static bool compat_handle() {
+  if (g_compat) return true;
+  wk_config cfg = {WK_MODE_ESP_MFCC, WK_PREC_FP32, 1, 0, 0};
+  if (wk_create(&cfg, nullptr, &g_compat) != WK_OK) {
+    fprintf(stderr, "E (MFCC) device init failed: %s\n", wk_last_error());
+    return false;
   }
-  if (sampling_rate != 16000 || frame_size != 320 || hop_size != 256 || n_fft != 512 || n_filters != 40 ||
-      n_mfcc != 13) {
-    fprintf(stderr, "E (MFCC) unsupported configuration (supported: 16000/320/256/512/40/13)\n");
-    return nullptr;
-  }
-  std::lock_guard<std::mutex> lock(g_compat_mu);
-  if (!g_compat) {
-    wk_config cfg = {WK_MODE_ESP_MFCC, WK_PREC_FP32, 1, 0, 0};
-    if (wk_create(&cfg, nullptr, &g_compat) != WK_OK) {
-      fprintf(stderr, "E (MFCC) device init failed: %s\n", wk_last_error());
-      return nullptr;
-    }
-  }
-  const int nf = (signal_len - frame_size) / hop_size + 1;
-  float* host_out = (float*)malloc(sizeof(float) * (size_t)nf * n_mfcc);
-  if (!host_out) return nullptr;
-  float *d_sig = nullptr, *d_out = nullptr;
-  bool ok = false;
-  wk_status st = on_device(0, [&]() -> wk_status {
-    if (hipMalloc(&d_sig, sizeof(float) * signal_len) != hipSuccess) return WK_ERR_NO_MEMORY;
-    if (hipMalloc(&d_out, sizeof(float) * (size_t)nf * n_mfcc) != hipSuccess) return WK_ERR_NO_MEMORY;
-    if (hipMemcpy(d_sig, signal, sizeof(float) * signal_len, hipMemcpyHostToDevice) != hipSuccess) return WK_ERR_HIP;
-    wk_status s = wk_mfcc(g_compat, d_sig, WK_DTYPE_F32, 1, signal_len, signal_len, d_out, nullptr);
-    if (s != WK_OK) return s;
-    if (hipMemcpy(host_out, d_out, sizeof(float) * (size_t)nf * n_mfcc, hipMemcpyDeviceToHost) != hipSuccess)
-      return WK_ERR_HIP;
-    ok = true;
-    return WK_OK;
-  });
-  on_device(0, [&]() -> wk_status {
-    if (d_sig) (void)hipFree(d_sig);
-    if (d_out) (void)hipFree(d_out);
-    return WK_OK;
-  });
-  if (st != WK_OK || !ok) {
-    fprintf(stderr, "E (MFCC) extract_mfcc failed: %s\n", wk_last_error());
-    free(host_out);
-    return nullptr;
-  }
-  return host_out;
+  return true;
 }
 
-void free_mfcc(float* mfcc) { free(mfcc); }
+// Every other parameter set: wk_esp_mfcc objects, cached per parameter set
+// (mfcc.c rebuilds its tables per call; the single-frame variant caches its
+// filterbank per (sr, n_filters, n_fft), mfcc.c:362-377).  Caller holds g_compat_mu.
+struct EspKey {
+  int sr, frame, n_fft, n_filters, n_mfcc;
+  bool operator==(const EspKey& o) const {
+    return sr == o.sr && frame == o.frame && n_fft == o.n_fft && n_filters == o.n_filters && n_mfcc == o.n_mfcc;
+  }
+};
+static std::vector<std::pair<EspKey, wk_esp_mfcc*>> g_esp_cache;
+static wk_esp_mfcc* esp_object(const EspKey& k) {
+  for (auto& e : g_esp_cache)
+    if (e.first == k) return e.second;
+  wk_esp_mfcc* m = nullptr;
+  if (wk_esp_mfcc_create(k.sr, k.frame, k.n_fft, k.n_filters, k.n_mfcc, 1, 0, &m) != WK_OK) return nullptr;
+  if (g_esp_cache.size() >= 8) {   // oldest out
+    (void)wk_esp_mfcc_destroy(g_esp_cache.front().second);
+    g_esp_cache.erase(g_esp_cache.begin());
+  }
+  g_esp_cache.emplace_back(k, m);
+  return m;
+}
 
-// mfcc.c:297-427 flow_extract_mfcc_single_frame: one frame, NO pre-emphasis,
-// symmetric Hamming over frame_size, |FFT|^2/n_fft + 1e-12 (esp-dsp packing),
-// mel, ln, DCT-II -> malloc'd n_mfcc floats (free with free_mfcc), NULL on bad
-// arguments (mfcc.c:300-303).  GPU-backed like extract_mfcc; the reference
-// configuration (320-sample frame, 16 kHz, 512, 40 filters, n_mfcc <= 13) only.
-float* flow_extract_mfcc_single_frame(const float* frame, int frame_size, int sampling_rate, int n_fft, int n_filters,
-                                      int n_mfcc) {
-  if (!frame || frame_size <= 0 || frame_size > n_fft) {
-    fprintf(stderr, "E (MFCC) Invalid frame parameters\n");
-    return nullptr;
-  }
-  if (sampling_rate != 16000 || frame_size != 320 || n_fft != 512 || n_filters != 40 || n_mfcc < 1 || n_mfcc > 13) {
-    fprintf(stderr, "E (MFCC) unsupported configuration (supported: 320-sample frame, 16000/512/40, n_mfcc <= 13)\n");
-    return nullptr;
-  }
-  std::lock_guard<std::mutex> lock(g_compat_mu);
-  if (!g_compat) {
-    wk_config cfg = {WK_MODE_ESP_MFCC, WK_PREC_FP32, 1, 0, 0};
-    if (wk_create(&cfg, nullptr, &g_compat) != WK_OK) {
-      fprintf(stderr, "E (MFCC) device init failed: %s\n", wk_last_error());
-      return nullptr;
-    }
-  }
-  float* host_out = (float*)malloc(sizeof(float) * (size_t)n_mfcc);
+// Host signal -> malloc'd host [nf][n_mfcc] through the device: `run` fills
+// d_out from d_sig.  Caller holds g_compat_mu.
+template <class F>
+static float* shim_run(const float* signal, int n_in, size_t n_out, const char* what, F run) {
+  float* host_out = (float*)malloc(sizeof(float) * (n_out ? n_out : 1));
   if (!host_out) return nullptr;
-  float tmp[13];
   float *d_sig = nullptr, *d_out = nullptr;
-  wk_status st = on_device(0, [&]() -> wk_status {
+  const wk_status st = on_device(0, [&]() -> wk_status {
     hipError_t e;
-    if ((e = hipMalloc(&d_sig, sizeof(float) * frame_size)) != hipSuccess) return hip_fail(e, "hipMalloc");
-    if ((e = hipMalloc(&d_out, sizeof(float) * 13)) != hipSuccess) return hip_fail(e, "hipMalloc");
-    if ((e = hipMemcpy(d_sig, frame, sizeof(float) * frame_size, hipMemcpyHostToDevice)) != hipSuccess)
+    if ((e = hipMalloc(&d_sig, sizeof(float) * n_in)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if ((e = hipMalloc(&d_out, sizeof(float) * (n_out ? n_out : 1))) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if ((e = hipMemcpy(d_sig, signal, sizeof(float) * n_in, hipMemcpyHostToDevice)) != hipSuccess)
       return hip_fail(e, "H2D");
-    if ((e = wk::launch_frontend(false, false, d_sig, 1, frame_size, frame_size, d_out, 1, 0, 1, 0.0f, nullptr)) !=
-        hipSuccess)
-      return hip_fail(e, "frontend launch");
-    if ((e = hipMemcpy(tmp, d_out, sizeof(float) * 13, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "D2H");
+    const wk_status s = run(d_sig, d_out);
+    if (s != WK_OK) return s;
+    if ((e = hipMemcpy(host_out, d_out, sizeof(float) * n_out, hipMemcpyDeviceToHost)) != hipSuccess)
+      return hip_fail(e, "D2H");
     return WK_OK;
   });
   on_device(0, [&]() -> wk_status {
@@ -449,12 +427,82 @@ float* flow_extract_mfcc_single_frame(const float* frame, int frame_size, int sa
     return WK_OK;
   });
   if (st != WK_OK) {
-    fprintf(stderr, "E (MFCC) flow_extract_mfcc_single_frame failed: %s\n", wk_last_error());
+    fprintf(stderr, "E (MFCC) %s failed: %s\n", what, wk_last_error());
     free(host_out);
     return nullptr;
   }
-  memcpy(host_out, tmp, sizeof(float) * (size_t)n_mfcc);
   return host_out;
+}
+
+extern "C" {
+
+float* extract_mfcc(const float* signal, int signal_len, int sampling_rate, int frame_size, int hop_size, int n_fft,
+                    int n_filters, int n_mfcc) {
+  // mfcc.c:434-437: NULL signal or a signal shorter than one frame -> NULL.
+  if (!signal || signal_len < frame_size || frame_size <= 0) {
+    fprintf(stderr, "E (MFCC) Invalid signal parameters\n");
+    return nullptr;
+  }
+  if (hop_size < 1) {   // (mfcc.c:447 divides by it)
+    fprintf(stderr, "E (MFCC) Invalid hop size\n");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(g_compat_mu);
+  const int nf = (signal_len - frame_size) / hop_size + 1;
+  const size_t n_out = (size_t)nf * n_mfcc;
+  if (sampling_rate == 16000 && frame_size == 320 && hop_size == 256 && n_fft == 512 && n_filters == 40 &&
+      n_mfcc == 13) {
+    if (!compat_handle()) return nullptr;
+    return shim_run(signal, signal_len, n_out, "extract_mfcc", [&](float* d_sig, float* d_out) {
+      return wk_mfcc(g_compat, d_sig, WK_DTYPE_F32, 1, signal_len, signal_len, d_out, nullptr);
+    });
+  }
+  wk_esp_mfcc* m = esp_object({sampling_rate, frame_size, n_fft, n_filters, n_mfcc});
+  if (!m) {
+    fprintf(stderr, "E (MFCC) unsupported configuration: %s\n", wk_last_error());
+    return nullptr;
+  }
+  return shim_run(signal, signal_len, n_out, "extract_mfcc", [&](float* d_sig, float* d_out) {
+    return wk_esp_mfcc_run(m, d_sig, 1, signal_len, signal_len, hop_size, 0.97f, d_out, nullptr);
+  });
+}
+
+void free_mfcc(float* mfcc) { free(mfcc); }
+
+// mfcc.c:297-427 flow_extract_mfcc_single_frame: one frame, NO pre-emphasis,
+// symmetric Hamming over frame_size, |FFT|^2/n_fft + 1e-12 (esp-dsp packing),
+// mel, ln, DCT-II -> malloc'd n_mfcc floats (free with free_mfcc), NULL on bad
+// arguments (mfcc.c:300-303).  The reference configuration (320-sample frame,
+// 16 kHz, 512, 40 filters, n_mfcc <= 13) runs on the fixed-geometry kernel,
+// any other on wk_esp_mfcc.
+float* flow_extract_mfcc_single_frame(const float* frame, int frame_size, int sampling_rate, int n_fft, int n_filters,
+                                      int n_mfcc) {
+  if (!frame || frame_size <= 0 || frame_size > n_fft) {
+    fprintf(stderr, "E (MFCC) Invalid frame parameters\n");
+    return nullptr;
+  }
+  if (n_mfcc < 1) {
+    fprintf(stderr, "E (MFCC) Invalid n_mfcc\n");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(g_compat_mu);
+  if (sampling_rate == 16000 && frame_size == 320 && n_fft == 512 && n_filters == 40 && n_mfcc <= 13) {
+    if (!compat_handle()) return nullptr;
+    float* all = shim_run(frame, frame_size, 13, "flow_extract_mfcc_single_frame", [&](float* d_sig, float* d_out) {
+      const hipError_t e = wk::launch_frontend(false, false, d_sig, 1, frame_size, frame_size, d_out, 1, 0, 1, 0.0f,
+                                               nullptr);
+      return e == hipSuccess ? WK_OK : hip_fail(e, "frontend launch");
+    });
+    return all;   // (the first n_mfcc of the 13 are the caller's; the block is larger than it needs)
+  }
+  wk_esp_mfcc* m = esp_object({sampling_rate, frame_size, n_fft, n_filters, n_mfcc});
+  if (!m) {
+    fprintf(stderr, "E (MFCC) unsupported configuration: %s\n", wk_last_error());
+    return nullptr;
+  }
+  return shim_run(frame, frame_size, (size_t)n_mfcc, "flow_extract_mfcc_single_frame", [&](float* d_sig, float* d_out) {
+    return wk_esp_mfcc_run(m, d_sig, 1, frame_size, frame_size, frame_size, 0.0f, d_out, nullptr);
+  });
 }
 
 // mfcc.c:530-553: min/max/avg over the finite entries.

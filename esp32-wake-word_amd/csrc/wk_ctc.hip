@@ -650,9 +650,14 @@ __global__ __launch_bounds__(1024) void ctc_zscore_kernel(float* __restrict__ fe
 // folds the log-mel passes' {S, Q} partials (ctc_logmel_fft2_kernel<true>) in
 // double into zs[b] = {mean, 1/std} (unbiased std, ctc.py:101-104), or {0, 1}
 // when std is 0 (no normalisation).  Needs T >= 6: a pass then spans at most
-// two utterances.
-__global__ __launch_bounds__(256) void ctc_zstats_kernel(const float4* __restrict__ part, int64_t batch, int T,
-                                                         float2* __restrict__ zs) {
+// two utterances.  The partials are float sums, so Q - S m carries ~1e-6 of
+// Q's size in rounding: a variance at or below 1e-5 of the mean square (a
+// constant utterance, silent or not, lands there) is recomputed exactly from
+// the utterance's raw rows, two passes in double -- a constant utterance then
+// gets std 0 exactly and stays un-normalised, as ctc.py:104's `std() > 0` test
+// leaves it.
+__global__ __launch_bounds__(256) void ctc_zstats_kernel(const float4* __restrict__ part, const float* __restrict__ feats,
+                                                         int64_t batch, int T, float2* __restrict__ zs) {
   // one wave per utterance: lane i takes passes p0 + i, + 64, ...
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -670,9 +675,29 @@ __global__ __launch_bounds__(256) void ctc_zstats_kernel(const float4* __restric
     S += __shfl_xor(S, o, 64);
     Q += __shfl_xor(Q, o, 64);
   }
-  const double n = (double)T * kMels, m = S / n, var = (Q - S * m) / (n - 1.0);
+  const double n = (double)T * kMels;
+  double m = S / n, var = (Q - S * m) / (n - 1.0);
+  m += (double)wk_logf(1e-8f);   // S, Q are sums of x - ln(1e-8)
+  // (Q == 0: every value is the floor ln(1e-8), digital silence: std 0 as it stands)
+  if (Q > 0.0 && var <= 1e-5 * (Q / n)) {   // (wave-uniform) within the partials' rounding: exact two-pass statistics
+    const float* f = feats + r0 * kMels;
+    const int64_t cnt = (int64_t)T * kMels;
+    double s1 = 0.0;
+    for (int64_t i = lane; i < cnt; i += 64) s1 += (double)f[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s1 += __shfl_xor(s1, o, 64);
+    m = s1 / n;
+    double s2 = 0.0;
+    for (int64_t i = lane; i < cnt; i += 64) {
+      const double d = (double)f[i] - m;
+      s2 += d * d;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+    var = s2 / (n - 1.0);
+  }
   const float sd = var > 0.0 ? (float)sqrt(var) : 0.0f;
-  if (lane == 0) zs[b] = sd > 0.0f ? make_float2(wk_logf(1e-8f) + (float)m, 1.0f / sd) : make_float2(0.0f, 1.0f);
+  if (lane == 0) zs[b] = sd > 0.0f ? make_float2((float)m, 1.0f / sd) : make_float2(0.0f, 1.0f);
 }
 
 // ---------------------------------------------------------------------------
@@ -1801,9 +1826,13 @@ __device__ unsigned long long g_out_stamps[kOutWaves][16];
 #define OUT_HIT(k) do {} while (0)
 #endif
 // KEYED (V <= 4096, so 4 NT <= 256): the running maximum carries its column
-// in the value's low 8 mantissa bits (the tag 255 - (4 tile + cf); the column
-// is 16 (4 tile + cf) + li), so the epilogue is one v_and_or_b32 per value and
-// one v_max3_f32 per two values instead of compare + two selects per value.
+// in the value's low 8 mantissa bits, so the epilogue is two VALU per value
+// and one v_max3_f32 per two values instead of compare + two selects per
+// value.  The tag is 255 - (4 tile + cf) for a positive value and 4 tile + cf
+// for a negative one (v_perm_b32 spreads the sign bit over the low byte, the
+// XOR with the tag finishes it): an earlier column then always makes the
+// larger tagged value, whichever the sign, so equal logits keep the first
+// index, as torch.argmax does (ctc.py:454).  The column is 16 (4 tile + cf) + li.
 // A tagged value moves by < 2^-15 of itself: the first maximum is exact except
 // between logits that agree to within that (fp16 operands already put ~1e-3 of
 // noise on every logit); the tokens stay a function of the row alone.
@@ -1818,8 +1847,15 @@ __device__ __forceinline__ float out_max3(float m, float k0, float k1) {
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(k0), "v"(k1));
   return r;
 }
-__device__ __forceinline__ float out_tag(float x, unsigned mask, unsigned tag) {
-  return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, x) & mask) | tag);
+// sel = 0x03020109: bytes 3..1 of x, byte 0 = x's sign bit replicated (v_perm_b32 selector 9)
+__device__ __forceinline__ float out_tag(float x, unsigned sel, unsigned tag) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  return __builtin_bit_cast(float, __builtin_amdgcn_perm(u, u, sel) ^ tag);
+}
+// The column block (4 tile + cf) of a tagged value.
+__device__ __forceinline__ int out_untag(float m) {
+  const unsigned u = __builtin_bit_cast(unsigned, m);
+  return (int)(((u & 255u) ^ ((u >> 31) ? 0u : 255u)));
 }
 template <bool LOGITS, bool KEYED>
 __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const __half* __restrict__ y,
@@ -1944,8 +1980,8 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   __syncthreads();
   float mx[kOutRF][4];
   int ix[kOutRF][4];
-  unsigned kmask;   // (KEYED) 0xFFFFFF00 in a VGPR the compiler cannot fold: one v_and_or_b32
-  asm("v_mov_b32 %0, 0xffffff00" : "=v"(kmask));   // per tag (a literal mask would split it in two)
+  unsigned ksel;   // (KEYED) the v_perm_b32 selector of out_tag, in a VGPR (VOP3 takes no literal)
+  asm("v_mov_b32 %0, 0x03020109" : "=v"(ksel));
 #pragma unroll
   for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
@@ -2007,7 +2043,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
                 x0 = v - 16 < V ? x0 : -FLT_MAX;
                 x1 = v < V ? x1 : -FLT_MAX;
               }
-              mx[rf][i] = out_max3(mx[rf][i], out_tag(x0, kmask, tag + 1), out_tag(x1, kmask, tag));
+              mx[rf][i] = out_max3(mx[rf][i], out_tag(x0, ksel, tag + 1), out_tag(x1, ksel, tag));
             }
         }
       } else if (decltype(full)::value || v < V) {
@@ -2196,7 +2232,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float m = mx[rf][i];
-      int k = KEYED ? 16 * (255 - (int)(__builtin_bit_cast(unsigned, m) & 255u)) + li : ix[rf][i];
+      int k = KEYED ? 16 * out_untag(m) + li : ix[rf][i];
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
         const float om = __shfl_xor(m, o, 64);
@@ -2691,7 +2727,8 @@ wk_status ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n
     if (s == WK_OK)
       s = timed(c, WK_CTC_STAGE_ZSCORE, st, [&]() -> wk_status {
         if (part)
-          hipLaunchKernelGGL(ctc_zstats_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, part, batch, T, zs);
+          hipLaunchKernelGGL(ctc_zstats_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, part, d_feats, batch, T,
+                             zs);
         else
           hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
         return WK_OK;

@@ -5,16 +5,6 @@
 #include "wk_common.h"
 #include "wk_tables.h"
 
-#ifndef WK_SPLIT_G
-#define WK_SPLIT_G 3   // real-FFT split chains interleaved per group (fe_rest)
-#endif
-#ifndef WK_SPLIT_MIRROR
-#define WK_SPLIT_MIRROR 0   // 1: second-pass columns placed so real-FFT split partners are row mirrors (one DPP)
-#endif
-#ifndef WK_TW_GROUP
-#define WK_TW_GROUP 0   // >0: fence the twiddle LDS reads into groups of this many (0 = compiler schedules; measured equal)
-#endif
-
 namespace wk {
 
 // W32^k2 = exp(-2*pi*i*k2/32), k2 = 0..8.
@@ -119,16 +109,6 @@ __device__ __forceinline__ void load_raw_part(__amdgpu_buffer_rsrc_t rs, int bas
   if (part == 0) r.xb = raw_ld<T>(rs, base - 1);
 }
 
-// Column k1 of the second DFT16 pass held by lane j of a 16-lane group.
-// Plain: k1 = j; the split partner column 16 - k1 then sits in lane 16 - j
-// (two DPP moves).  Mirrored (WK_SPLIT_MIRROR): columns 1-7 in lanes 1-7,
-// 9-15 in lanes 8-14, 0 in lane 0, 8 in lane 15 -- the partner of the column
-// in lane j is in lane 15 - j (DPP row_mirror), and the two self-partnered
-// columns 0 and 8 sit in lanes 0 and 15.
-__device__ __forceinline__ constexpr int fe_kcol(int j) {
-  return WK_SPLIT_MIRROR ? (j < 8 ? j : (j == 15 ? 8 : j + 1)) : j;
-}
-
 struct NoPrefetch {
   __device__ __forceinline__ void operator()(int) const {}
 };
@@ -140,15 +120,41 @@ __device__ __forceinline__ float row_rol1(float v) {  // lane l <- lane (l+1) mo
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x12F, 0xF, 0xF, false));
 }
 
-// LDS tables shared by the workgroup.
+// LDS tables shared by the workgroup (fe_init_tables).
 struct FeTables {
-  const float* win;   // [320] analysis window (mode-specific)
-  const float* tw;    // [15][16][2]: W256^(j*k1), k1 = 1..15
-  const float* tws;   // [7][16][2]: W512^(fe_kcol(j) + 16*k2), k2 = 1..7 (TWS kernels only), else null
+  const float* win;   // [320] analysis window, odd rows n1 negated in lanes j >= 8 (kWinB / kWinA)
+  const float* tw;    // [16 slots][16 lanes][2]: W256^(j * (s ^ (j & 8)))
 };
 
-// Fill the combined split twiddles of FeTables::tws (all threads of the WG).
-__device__ __forceinline__ void fe_init_tws(float* tws, int tid, int nthreads);
+// Split twiddles tws(k2, j) = fe_split_tw(j, k2), k2 = 1..7: the [7][16] f2 table in LDS.
+struct TwsLds {
+  const float* p;
+  __device__ __forceinline__ f2 operator()(int k2, int j) const {
+    return *reinterpret_cast<const f2*>(p + ((k2 - 1) * 16 + j) * 2);
+  }
+};
+
+// The real-FFT split pairs bin k = j + 16 k2 (lane j, register k2) with bin
+// 256 - k (lane (16 - j) & 15).  After the one-pass transpose of fe_rest the
+// lanes j >= 8 hold (-1)^k2 Z[k]; when a lane and its partner hold their
+// values with opposite signs, S and D of the split trade places, and the
+// twiddle -conj(W) in place of W restores |U|^2 and |U'|^2 exactly:
+//   D - i(-conj W) S = i conj(W) (S - i W D),  D + i(-conj W) S = -i conj(W) (S + i W D).
+__device__ __forceinline__ bool fe_split_flip(int j, int k2) {
+  return j == 8 || (j >= 1 && j <= 7 && !(k2 & 1)) || (j >= 9 && (k2 & 1));
+}
+__device__ __forceinline__ f2 fe_split_tw(int j, int k2) {   // W512^(j + 16 k2), or -conj of it
+  float sn, cs;
+  sincospif(-(float)(j + 16 * k2) / 256.0f, &sn, &cs);
+  return fe_split_flip(j, k2) ? f2{-cs, sn} : f2{cs, sn};
+}
+__device__ __forceinline__ void fe_init_tws(float* tws, int tid, int nthreads) {
+  for (int i = tid; i < 7 * 16; i += nthreads) {
+    const f2 w = fe_split_tw(i % 16, i / 16 + 1);
+    tws[2 * i] = w.x;
+    tws[2 * i + 1] = w.y;
+  }
+}
 
 // Stage 0: pre-emphasis + window of the 320 frame samples as 160 complex
 // (even, odd) pairs: lane j holds pair index 16*n1 + j, n1 = 0..9.
@@ -207,84 +213,78 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
 
 // Stages 1..4 of one frame -> its power row (bins 0..256) in LDS.  All
 // complex arithmetic is packed fp32 (see f2 in wk_common.h).
+// xs: 8-byte aligned transpose scratch of 270 floats inside the frame's row
+// (row + 0 or row + 1; kPRow = 271).
+// w0: fe_split_tw(j, 0); tws(k2, j): fe_split_tw(j, k2), k2 = 1..7.
 // pf(k), k = 0..3, is called at four points of the round (prefetch parts);
-// pf(-1) just before the round's first write into `row`.
-// TWS: the split's twiddle W512^k, k = kc + 16 k2, is one table value per
-// (lane, k2) (tb.tws) instead of W512^kc x the constant W32^k2 -- one complex
-// multiply instead of two; bin 128 comes from |Z[128]|^2 directly.
-template <bool MODE_B, typename PF = NoPrefetch, bool TWS = false>
-__device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __restrict__ row, const FeTables& tb,
-                                        f2 w512, int esp_pack, const PF& pf = PF() WK_SP_PARAM) {
+// pf(-1) just before the round's first write into the row.
+//
+// 256-point complex FFT of the 160 (even, odd) sample pairs, four-step 16 x 16:
+//   Z[k1 + 16 k2] = sum_n2 W16^(n2 k2) W256^(n2 k1) sum_n1 W16^(n1 k1) z[16 n1 + n2]
+// with lane j = n2 for the first DFT16 and lane kc = k1 for the second.
+// One-pass transpose of {re, im} pairs: with h = j & 8 the lanes j >= 8 hold
+// their first-pass outputs in slot order k1 ^ 8 (their window rows n1 odd are
+// negated: A[k1 ^ 8] = sum_n1 (-1)^n1 W16^(n1 k1) a[n1]), so every lane's
+// slots 0-7 are the 8x8 blocks on the diagonal ((n2, k1) in the same half)
+// and slots 8-15 the off-diagonal blocks.  Each half is 128 complex values;
+// element (n2, k1) of the diagonal half sits at f2 index 17 (n2 & 7) + k1,
+// of the other at 17 (n2 & 7) + (k1 ^ 8): lane-uniform immediate offsets for
+// the writes (base 17 (j & 7) + h, offset s) and the reads (base kc or kc ^ 8,
+// offset 17 s), each 16 lanes on 16 distinct 8-byte bank pairs, and 135
+// f2 = 270 floats, inside the frame's own row.  Per round: 8 ds_write2_b64 +
+// 8 ds_read2_b64 (the re / im two-pass transpose was 16 write2 + 32 reads).
+// The second DFT16 then sees its inputs rotated by 8 in lanes kc >= 8, which
+// multiplies Z[kc + 16 k2] by (-1)^k2 there; fe_split_tw absorbs the sign.
+template <bool MODE_B, typename PF, typename TWS>
+__device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ row, float* __restrict__ xs,
+                                        const FeTables& tb, f2 w0, const TWS& tws, int esp_pack,
+                                        const PF& pf WK_SP_PARAM) {
   pf(0);
-#ifndef WK_ABL_NODFT   // WK_ABL_*: timing ablations of tools/debug (wrong results)
-  dft16(a);  // A[k1] at a[dft16_out(k1)]
-#endif
+  dft16(a);  // slot s: A[s ^ (j & 8)] at a[dft16_out(s)]
   WK_FE_HIT(2);
 
-  // twiddle W256^(j*k1) + 16x16 transpose through this frame's LDS row (pitch 17).
-  // (twiddles are applied in groups of 4 so their LDS reads do not all
-  // sit in VGPRs at once; re parts go straight to the transpose image.)
-  f2 b[16];
-  pf(-1);   // the first write into this frame's LDS row follows (fused kernel: wait until the row is free)
-  b[0] = a[0];
-  row[j] = b[0].x;
+  // twiddle W256^(n2 k1), n2 = j, k1 = s ^ (j & 8); each half is twiddled
+  // just before it is written (fewer live registers)
+  f2* x2 = reinterpret_cast<f2*>(xs);
+  const int wb = 17 * (j & 7) + (j & 8);
+  auto tw = [&](int s) { return cmul2(a[dft16_out(s)], *reinterpret_cast<const f2*>(tb.tw + (s * 16 + j) * 2)); };
+  f2 b[8];
 #pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) {
-#ifdef WK_ABL_NOTW
-    const f2 w = f2{0.5f, 0.25f};
-#else
-    const f2 w = *reinterpret_cast<const f2*>(tb.tw + ((k1 - 1) * 16 + j) * 2);
-#endif
-    b[k1] = cmul2(a[dft16_out(k1)], w);
-    row[17 * k1 + j] = b[k1].x;
-    if (WK_TW_GROUP > 0 && (k1 % (WK_TW_GROUP > 0 ? WK_TW_GROUP : 1)) == WK_TW_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
-  }
+  for (int s = 0; s < 8; ++s) b[s] = tw(s);
+  pf(-1);   // the first write into this frame's LDS row follows (fused kernel: wait until the row is free)
+#pragma unroll
+  for (int s = 0; s < 8; ++s) x2[wb + s] = b[s];
   WK_FE_HIT(3);
   pf(1);
   f2 c[16];
-#ifdef WK_ABL_NOTRANS
-  const int kc = fe_kcol(j);
-#pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) c[n2] = b[n2];
-#else
-  const int kc = fe_kcol(j);   // the column this lane transforms in the second pass
-  // The reads are single-dword (volatile: not merged into ds_read2_b32, whose
-  // two consecutive destination registers hold two elements' re parts and
-  // cost ~24 v_mov per round to re-pair as {re, im}); each lands in its half
-  // of c[n2] directly.
-  typedef const volatile __attribute__((address_space(3))) float lds_cvf;
-  lds_cvf* vrow = (lds_cvf*)(row + 17 * kc);
   wave_lds_sync();
 #pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) c[n2].x = vrow[n2];
+  for (int s = 0; s < 8; ++s) c[s] = x2[j + 17 * s];
+#pragma unroll
+  for (int s = 8; s < 16; ++s) b[s - 8] = tw(s);
   wave_lds_sync();
 #pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) row[17 * k1 + j] = b[k1].y;
+  for (int s = 8; s < 16; ++s) x2[wb + s - 8] = b[s - 8];
   wave_lds_sync();
 #pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) c[n2].y = vrow[n2];
+  for (int s = 8; s < 16; ++s) c[s] = x2[(j ^ 8) + 17 * (s - 8)];
   wave_lds_sync();
-#endif
   WK_FE_HIT(4);
 
   pf(2);
-#ifndef WK_ABL_NODFT
-  dft16(c);  // Z[j + 16*k2] at c[dft16_out(k2)]
-#endif
+  dft16(c);  // +-Z[j + 16*k2] at c[dft16_out(k2)]
   pf(3);
   WK_FE_HIT(5);
 
-  // Real-FFT split, k = j + 16*k2 (k2 = 0..8), with the partner Z[256 - k]:
+  // Real-FFT split, k = j + 16*k2 (k2 = 0..7), with the partner Z[256 - k]:
   //   S = Z[k] + conj Z[256-k],  D = Z[k] - conj Z[256-k],  bb = W512^k D,
   //   U = 2 X[k] = S - i bb,  U' = conj(2 X[256-k]) = S + i bb
   // (mode B folds the 1/4 of |X|^2 = |U|^2/4 into the filterbank weights).
   // {|U|^2, |U'|^2} is one packed pair: {Ux, U'x}^2 + {Uy, U'y}^2.
   // Partner: lane (16-j)&15 of this group, register 15-k2, fetched by two DPP
-  // row moves (row_mirror: j <- 15-j, then row_ror:1: j <- j-1), no LDS trip;
-  // lane 0 holds its own partner in register (16-k2)&15.
-#ifdef WK_SPLIT_BPERMUTE
-  const int src = ((lane & 48) | ((16 - j) & 15)) << 2;
-#endif
+  // row moves (row_mirror: j <- 15-j, then row_shr:1: j <- j-1), no LDS trip;
+  // lane 0 holds its own partner in register (16-k2)&15.  The twiddle is one
+  // value per (lane, k2) (w0 / tws), sign-adjusted by fe_split_tw.
   f2 sc0 = {1.0f, 1.0f}, sc = {1.0f, 1.0f};
   if constexpr (!MODE_B) {
     // mfcc.c:267 power = |X|^2 / n_fft + 1e-12 = |U|^2 / 2048 + 1e-12; the
@@ -294,76 +294,44 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
     sc = f2{e, e};
     sc0 = esp_pack ? (j == 0 ? f2{1.0f / 2048.0f, 0.0f} : sc) : sc;  // j==0, k2==0: bins 0 and 256
   }
-  // The nine k2 chains are ~20 dependent packed ops each; run them WK_SPLIT_G
-  // at a time, stage by stage, so independent ops fill each other's latency
-  // (left to itself the scheduler emitted them back to back, one chain at a
-  // time, with s_nop between dependent v_pk ops).
-#ifdef WK_ABL_NOSPLIT
-  row[j] = c[0].x + c[1].y + c[5].x + c[9].y + c[13].x;
-  return;
-#endif
-  constexpr int G = WK_SPLIT_G;
-  constexpr int K2MAX = TWS ? 7 : 8;
-  if constexpr (TWS) {
+  {
     // bin 128 (k2 = 8, column 0): X[128] = conj Z[128], so |U|^2 = 4 |Z[128]|^2.
     const f2 z = c[dft16_out(8)];
     float p128 = 4.0f * __builtin_fmaf(z.x, z.x, z.y * z.y);
     if constexpr (!MODE_B) p128 = __builtin_fmaf(p128, sc.x, 1e-12f);
     if (j == 0) row[128] = p128;
   }
+  // The eight k2 chains are ~20 dependent packed ops each; run them G at a
+  // time, stage by stage, so independent ops fill each other's latency
+  // (left to itself the scheduler emitted them back to back, one chain at a
+  // time, with s_nop between dependent v_pk ops).
+  constexpr int G = 3;
 #pragma unroll
-  for (int k0 = 0; k0 <= K2MAX; k0 += G) {
+  for (int k0 = 0; k0 < 8; k0 += G) {
     f2 S[G], D[G], pw[G];
 #pragma unroll
     for (int t = 0; t < G; ++t) {
       const int k2 = k0 + t;
-      if (k2 > K2MAX) continue;
+      if (k2 > 7) continue;
       const f2 zk = c[dft16_out(k2)];
+      const f2 sv = c[dft16_out(15 - k2)];
+      const f2 own = c[dft16_out((16 - k2) & 15)];
+      // row_mirror (lane j <- 15 - j), then row_shr:1 (lane j <- j - 1) with
+      // bound_ctrl off: lane 0 has no source and keeps `old` = its own
+      // partner register -- no lane select.
       f2 zq;
-      if (k2 < 8) {
-        const f2 sv = c[dft16_out(15 - k2)];
-        const f2 own = c[dft16_out((16 - k2) & 15)];
-#if WK_SPLIT_MIRROR
-        // lane 15 - j holds the partner column; lanes 0 (column 0) and 15
-        // (column 8) are their own partners: registers (16 - k2) & 15 / 15 - k2.
-        const float pr = dpp<0x140>(sv.x);
-        const float pi = dpp<0x140>(sv.y);
-        zq = j == 0 ? own : (j == 15 ? sv : f2{pr, pi});
-#else
-#ifdef WK_SPLIT_BPERMUTE
-        const float pr = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sv.x)));
-        const float pi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sv.y)));
-        zq = j == 0 ? own : f2{pr, pi};
-#else
-        // row_mirror (lane j <- 15 - j), then row_shr:1 (lane j <- j - 1) with
-        // bound_ctrl off: lane 0 has no source and keeps `old` = its own
-        // partner register -- no lane select.
-        zq.x = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.x), __float_as_int(dpp<0x140>(sv.x)),
-                                                          0x111, 0xF, 0xF, false));
-        zq.y = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), __float_as_int(dpp<0x140>(sv.y)),
-                                                          0x111, 0xF, 0xF, false));
-#endif
-#endif
-      } else {
-        zq = c[dft16_out(8)];
-      }
+      zq.x = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.x), __float_as_int(dpp<0x140>(sv.x)),
+                                                        0x111, 0xF, 0xF, false));
+      zq.y = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), __float_as_int(dpp<0x140>(sv.y)),
+                                                        0x111, 0xF, 0xF, false));
       S[t] = fma2(zq, f2{1.0f, -1.0f}, zk);
       D[t] = fma2(zq, f2{-1.0f, 1.0f}, zk);
     }
 #pragma unroll
     for (int t = 0; t < G; ++t) {
       const int k2 = k0 + t;
-      if (TWS || k2 > 8) continue;
-      if (k2 == 8) D[t] = swp(D[t]) * f2{1.0f, -1.0f};   // W32^8 = -i
-      else if (k2 > 0) D[t] = cmulc(D[t], w32(k2));
-    }
-#pragma unroll
-    for (int t = 0; t < G; ++t) {
-      const int k2 = k0 + t;
-      if (k2 > K2MAX) continue;
-      f2 wk = w512;
-      if (TWS && k2 > 0) wk = *reinterpret_cast<const f2*>(tb.tws + ((k2 - 1) * 16 + j) * 2);
-      const f2 bb = cmul2(D[t], wk);
+      if (k2 > 7) continue;
+      const f2 bb = cmul2(D[t], k2 == 0 ? w0 : tws(k2, j));
       const f2 uvx = fma2(by(bb), f2{1.0f, -1.0f}, bx(S[t]));
       const f2 uvy = fma2(bx(bb), f2{-1.0f, 1.0f}, by(S[t]));
       pw[t] = fma2(uvx, uvx, uvy * uvy);
@@ -372,14 +340,10 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, int lane, float* __r
 #pragma unroll
     for (int t = 0; t < G; ++t) {
       const int k2 = k0 + t;
-      if (k2 > K2MAX) continue;
-      const int kb = kc + 16 * k2;
-      if (k2 < 8) {
-        row[kb] = pw[t].x;
-        row[256 - kb] = pw[t].y;
-      } else if (j == 0) {
-        row[128] = pw[t].x;
-      }
+      if (k2 > 7) continue;
+      const int kb = j + 16 * k2;
+      row[kb] = pw[t].x;
+      row[256 - kb] = pw[t].y;
     }
   }
   WK_FE_HIT(6);
@@ -428,42 +392,35 @@ __device__ __forceinline__ void cmvn_lane2(float& v0, float& v1, bool valid, int
   v1 = d1 * (1.0f / (s1 + 1e-8f));
 }
 
-// LDS carve (floats): twiddles | window | log-mel [40][64] | power rows [63][271].
-constexpr int kTwOff = 0, kTwSize = 15 * 16 * 2;
-constexpr int kWinOff = kTwOff + kTwSize, kWinSize = 320;
-constexpr int kLOff = kWinOff + kWinSize, kLSize = 40 * WK_LSTRIDE;
+// LDS carve (floats): twiddles | split twiddles | log-mel [40][64] | power
+// rows [63][271] | window.  The standalone front-end stops before the window
+// (it reads the window from the constant table: kFeLdsNoWin keeps two
+// workgroups per CU); the fused kernel copies it to LDS.
+constexpr int kTwOff = 0, kTwSize = 16 * 16 * 2;
+constexpr int kTwsOff = kTwOff + kTwSize, kTwsSize = 7 * 16 * 2;
+constexpr int kLOff = kTwsOff + kTwsSize, kLSize = 40 * WK_LSTRIDE;
 constexpr int kPOff = kLOff + kLSize, kPSize = kNFramesB * kPRow;
-constexpr int kFeLds = kPOff + kPSize;
-static_assert(kFeLds * 4 <= 81920, "front-end LDS must allow 2 workgroups per CU");
+constexpr int kFeLdsNoWin = kPOff + kPSize;
+constexpr int kWinOff = (kFeLdsNoWin + 1) & ~1, kWinSize = 320;
+constexpr int kFeLds = kWinOff + kWinSize;
+static_assert(kFeLdsNoWin * 4 <= 81920, "standalone front-end LDS must allow 2 workgroups per CU");
+static_assert(kLOff % 4 == 0, "log-mel rows are read with ds_read_b128");
+static_assert(kPOff % 2 == 0 && kPRow % 2 == 1 && kPRow >= 271,
+              "row f's transpose scratch is row + (f & 1): 8-byte aligned, 270 floats");
 
-// Fill the window / twiddle tables of the LDS carve (all threads of the WG).
-template <bool MODE_B>
+// Fill the twiddle tables (and the window, WIN) of the LDS carve (all threads of the WG).
+template <bool MODE_B, bool WIN>
 __device__ __forceinline__ void fe_init_tables(float* smem, int tid, int nthreads) {
-  for (int i = tid; i < 320; i += nthreads) smem[kWinOff + i] = MODE_B ? kWinB[i] : kWinA[i];
-  for (int i = tid; i < 15 * 16; i += nthreads) {
-    const int k1 = i / 16 + 1, jj = i % 16;
+  if (WIN)
+    for (int i = tid; i < 320; i += nthreads) smem[kWinOff + i] = MODE_B ? kWinB[i] : kWinA[i];
+  for (int i = tid; i < 16 * 16; i += nthreads) {
+    const int s = i / 16, jj = i % 16, k1 = s ^ (jj & 8);
     float sn, cs;
     sincospif(-(float)(jj * k1) / 128.0f, &sn, &cs);
     smem[kTwOff + 2 * i] = cs;
     smem[kTwOff + 2 * i + 1] = sn;
   }
-}
-
-__device__ __forceinline__ f2 fe_w512(int j) {
-  float sn, cs;
-  sincospif(-(float)j / 256.0f, &sn, &cs);
-  return f2{cs, sn};
-}
-__device__ __forceinline__ f2 fe_w512_lane(int j) { return fe_w512(fe_kcol(j)); }   // W512^k1 of the lane's column
-
-__device__ __forceinline__ void fe_init_tws(float* tws, int tid, int nthreads) {
-  for (int i = tid; i < 7 * 16; i += nthreads) {
-    const int k2 = i / 16 + 1, jj = i % 16;
-    float sn, cs;
-    sincospif(-(float)(fe_kcol(jj) + 16 * k2) / 256.0f, &sn, &cs);
-    tws[2 * i] = cs;
-    tws[2 * i + 1] = sn;
-  }
+  fe_init_tws(smem + kTwsOff, tid, nthreads);
 }
 
 }  // namespace wk

@@ -38,16 +38,17 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
                                                                   int n_chunks, int nf, int win_len,
                                                                   int64_t clip_stride, float* __restrict__ out,
                                                                   int esp_pack, int cmvn, float pre) {
-  __shared__ __attribute__((aligned(16))) float smem[kFeLds];
+  __shared__ __attribute__((aligned(16))) float smem[kFeLdsNoWin];
   float* P = smem + kPOff;
   float* L = smem + kLOff;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, j = lane & 15;
 
-  fe_init_tables<MODE_B>(smem, threadIdx.x, kFeBlock);
-  const FeTables tb = {smem + kWinOff, smem + kTwOff, nullptr};
-  const f2 w512 = fe_w512_lane(j);
+  fe_init_tables<MODE_B, false>(smem, threadIdx.x, kFeBlock);
+  const FeTables tb = {MODE_B ? kWinB : kWinA, smem + kTwOff};   // window: constant table (L1-resident)
+  const TwsLds tws = {smem + kTwsOff};
+  const f2 w0 = fe_split_tw(j, 0);
   // Frame slots: groups 0/1 (and 2/3) of a wave take frames 16 apart so their
   // pitch-17 transpose images fall in disjoint LDS banks.
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(kFeBlock, 4) void wk_frontend_kernel(const T* __res
       }
       // pf is consumed: prefetch the next wave-round, (u,1) or (u+grid,0), into it.
       prefetch(r == 0 ? u : u + gridDim.x, r ^ 1, pf);
-      if (fl < nfc) fe_rest<MODE_B>(a, j, lane, P + fl * kPRow, tb, w512, esp_pack);
+      if (fl < nfc) fe_rest<MODE_B>(a, j, P + fl * kPRow, P + fl * kPRow + (fl & 1), tb, w0, tws, esp_pack, NoPrefetch());
     }
     wg_barrier_lds();
 

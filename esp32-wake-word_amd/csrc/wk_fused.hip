@@ -57,9 +57,6 @@ __device__ __forceinline__ void dbg_copy_logmel(float* dst, const float* lbuf, i
 #endif
 
 constexpr int NBF = 4;               // clips per CNN batch
-#ifndef WK_FE_TWS
-#define WK_FE_TWS 1                  // real-FFT split with the combined twiddle table (fe_rest TWS)
-#endif
 #ifndef WK_DCT_EAGER
 #define WK_DCT_EAGER 1               // MFMA DCT of the next batch's clips between this batch's conv phases
 #endif
@@ -108,9 +105,8 @@ static_assert(kF1Off % 4 == 0 && kF2Off % 4 == 0 && kB1Off % 2 == 0 && kB2Off % 
 enum { kConvF32 = 0, kConvBf16 = 1, kConvBf16x3 = 2 };
 // Scratch power row for the one frame slot past the clip (frame 63): its lanes
 // still run the FFT so that the prefetch loads issued inside fe_rest execute.
-constexpr int kDummyRowOff = kImgEnd;
-constexpr int kTwsOff = (kDummyRowOff + kPRow + 1) & ~1;   // combined split twiddles [7][16] f2 (8-byte aligned)
-constexpr int kFusedLds = kTwsOff + 7 * 16 * 2;
+constexpr int kDummyRowOff = (kImgEnd + 1) & ~1;          // even: its scratch is row + (63 & 1)
+constexpr int kFusedLds = kDummyRowOff + kPRow + 1;
 static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 
 // kCtrlLFree + w (w = CNN wave 0..7): clips whose log-mel buffer CNN wave w
@@ -229,8 +225,9 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   float* L1 = smem + kL1Off;
   unsigned* ctrl = reinterpret_cast<unsigned*>(smem + kCtrlOff);
   const int g = lane >> 4, j = lane & 15;
-  const FeTables tb = {smem + kWinOff, smem + kTwOff, WK_FE_TWS ? smem + kTwsOff : nullptr};
-  const f2 w512 = fe_w512_lane(j);
+  const FeTables tb = {smem + kWinOff, smem + kTwOff};
+  const TwsLds tws = {smem + kTwsOff};
+  const f2 w0 = fe_split_tw(j, 0);
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);
   const int fw = wave;   // frame slot of this wave (moving the edge frames to other waves measured neutral)
 #ifdef WK_ABL_NOEDGE
@@ -314,7 +311,7 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       };
       WK_STAMP(1);
       float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
-      fe_rest<true, decltype(pf_part), (bool)WK_FE_TWS>(a, j, lane, row, tb, w512, 0, pf_part WK_SP_ARG);
+      fe_rest<true>(a, j, row, row + (fl & 1), tb, w0, tws, 0, pf_part WK_SP_ARG);
     }
     if (exp_flags & 4) __builtin_amdgcn_s_setprio(1); else if (exp_flags & 8) __builtin_amdgcn_s_setprio(0);
 #ifndef WK_ABL_NOFEBAR
@@ -795,9 +792,8 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  fe_init_tables<true>(smem, tid, kFusedBlock);
-  if (WK_FE_TWS) fe_init_tws(smem + kTwsOff, tid, kFusedBlock);
-  for (int i = tid; i < kTwsOff - kGOff; i += kFusedBlock) smem[kGOff + i] = 0.0f;  // ctrl, guards, pads
+  fe_init_tables<true, true>(smem, tid, kFusedBlock);
+  for (int i = tid; i < kFusedLds - kGOff; i += kFusedBlock) smem[kGOff + i] = 0.0f;  // ctrl, guards, pads
   __syncthreads();
   const int64_t n_mine = batch > (int64_t)blockIdx.x ? (batch - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   // The front-end role is the critical path: static issue priority over the

@@ -187,8 +187,13 @@ def main():
            "// Constants restated from torchaudio (mode B) and main/esp_mfcc/mfcc.c (mode A).",
            "#pragma once", "", "#ifndef WK_LSTRIDE", "#define WK_LSTRIDE 64  // log-mel image is [mel][frame]", "#endif", ""]
     out.append(f"// nnz(mode B fbank) = {int((fbB != 0).sum())}, nnz(mode A fbank) = {int((fbA != 0).sum())}")
-    out.append("__constant__ float kWinB[320] = {" + ", ".join(f32(v) for v in wB) + "};")
-    out.append("__constant__ float kWinA[320] = {" + ", ".join(f32(v) for v in wA) + "};")
+    # The analysis windows in the front-end's lane layout (wk_fe_dev.h fe_rest):
+    # element i = sample i of the frame, lane j = (i % 32) // 2, row n1 = i // 32;
+    # negated where n1 is odd and j >= 8 (the one-pass transpose's slot order).
+    sgn = np.array([-1.0 if ((i % 32) // 2 >= 8 and (i // 32) % 2 == 1) else 1.0 for i in range(320)], np.float32)
+    out.append("// analysis windows, signed for the front-end's one-pass FFT transpose (fe_rest)")
+    out.append("__constant__ float kWinB[320] = {" + ", ".join(f32(v) for v in wB * sgn) + "};")
+    out.append("__constant__ float kWinA[320] = {" + ", ".join(f32(v) for v in wA * sgn) + "};")
     out.append("")
     # Mode B: P holds |U|^2 with U = 2 V  ->  fold the 1/4 into the weights (exact).
     out.append(emit_mel(fbB, "melB", "B", 0.25))

@@ -5,7 +5,7 @@ ml_models/src/extract_mfcc.py, the xiaoa.onnx artefact); every compute call
 runs a hand-written gfx950 HIP kernel from libwakeword.so.
 """
 from ._lib import WakewordError, lib  # noqa: F401
-from .api import (KWSModel, detect, extract_mfcc, load_onnx, load_wav, mfcc, normalize_mfcc, pack_weights,  # noqa: F401
+from .api import (EspMfcc, KWSModel, detect, extract_mfcc, load_onnx, load_wav, mfcc, normalize_mfcc, pack_weights,  # noqa: F401
                   pad_audio, synth_clips)
 from .onnx_reader import read_onnx, xiaoa_state_dict  # noqa: F401
 from .stream import (DecisionRule, DeviceDetector, FrameDecisionLoop, FrameWindow, StreamingDetector,  # noqa: F401

@@ -272,6 +272,39 @@ def extract_mfcc(signal: Iterable[float], signal_len: Optional[int] = None, samp
     return out
 
 
+class EspMfcc:
+    """mfcc.c's mode-A MFCC at any parameter set, batched on the GPU
+    (wk_esp_mfcc: tables built once per object with the reference's formulas,
+    main/esp_mfcc/mfcc.c:144-234,298-527).  ``m(signals, hop_size)`` maps a
+    (B, L) float batch to (B, (L - frame_size) // hop_size + 1, n_mfcc) on
+    device; pre_emphasis 0.97 is extract_mfcc's, 0 the single-frame variant's."""
+
+    def __init__(self, sampling_rate: int = 16000, frame_size: int = 320, n_fft: int = 512, n_filters: int = 40,
+                 n_mfcc: int = 13, esp_dsp_packing: bool = True, device: int = 0):
+        self.frame_size, self.n_mfcc, self.device = frame_size, n_mfcc, device
+        self._m = C.c_void_p()
+        check(lib().wk_esp_mfcc_create(sampling_rate, frame_size, n_fft, n_filters, n_mfcc, int(esp_dsp_packing),
+                                       device, C.byref(self._m)), "wk_esp_mfcc_create")
+
+    def __call__(self, signals, hop_size: int, pre_emphasis: float = 0.97):
+        torch = _torch()
+        x = _as_device(signals, torch.float32, self.device)
+        if x.dim() == 1:
+            x = x.unsqueeze(0)
+        B, L = x.shape
+        nf = (L - self.frame_size) // hop_size + 1 if L >= self.frame_size and hop_size > 0 else 0
+        out = torch.empty((B, max(nf, 0), self.n_mfcc), dtype=torch.float32, device=x.device)
+        check(lib().wk_esp_mfcc_run(self._m, C.c_void_p(x.data_ptr()), B, L, L, hop_size, pre_emphasis,
+                                    C.c_void_p(out.data_ptr()), _stream(torch, self.device)), "wk_esp_mfcc_run")
+        return out
+
+    def __del__(self):
+        m = getattr(self, "_m", None)
+        if m and m.value:
+            lib().wk_esp_mfcc_destroy(m)
+            self._m = C.c_void_p()
+
+
 _DEFAULT_MODELS: Dict[tuple, "KWSModel"] = {}
 
 

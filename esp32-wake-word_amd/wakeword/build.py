@@ -21,7 +21,7 @@ CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(PKG, "libwakeword.so")
 OBJDIR = os.path.join(ROOT, "build")
-SOURCES = ["wk_frontend.hip", "wk_fused.hip", "wk_misc.hip", "wk_api.hip", "wk_ctc.hip", "wk_wav.hip", "wk_int8.hip"]
+SOURCES = ["wk_frontend.hip", "wk_fused.hip", "wk_misc.hip", "wk_api.hip", "wk_ctc.hip", "wk_wav.hip", "wk_int8.hip", "wk_esp_mfcc.hip"]
 LIBS = ["-L/opt/rocm/lib", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]   # rocBLAS: plain GEMMs of the CTC head
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WK_OFFLOAD_ARCH", "gfx950")

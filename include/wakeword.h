@@ -300,19 +300,44 @@ const char* wk_status_string(wk_status s);
 const char* wk_last_error(void);
 int32_t wk_abi_version(void);
 
+/* ---- mode A at any parameter set (main/esp_mfcc/mfcc.c:144-234,298-527) ----
+ * mfcc.c accepts any sampling rate, frame, hop, n_fft, n_filters and n_mfcc
+ * and rebuilds its filterbank, window and DCT tables per call.  A
+ * wk_esp_mfcc object holds one parameter set's tables on `device` (built
+ * with the reference's float formulas); wk_esp_mfcc_run computes, on the
+ * GPU, batch signals of signal_len samples (signal i at d_signal + i*stride)
+ * -> d_out[batch][n_frames][n_mfcc], n_frames = (signal_len - frame_size) /
+ * hop_size + 1: pre-emphasis `pre_emphasis` (0.97 in extract_mfcc, 0 in the
+ * single-frame variant), symmetric Hamming (alpha 0.53836), the frame in the
+ * first min(frame_size, n_fft) points of an n_fft-point FFT, power /n_fft +
+ * 1e-12 (esp_dsp_packing: dsps_cplx2reC_fc32's packing), mel, ln(max(E,1e-12)),
+ * DCT-II; coefficients past n_filters are 0 (mfcc.c's calloc).
+ * Domain: n_fft a power of two in [2, 4096] (esp-dsp's FFT refuses other
+ * lengths), 1 <= n_filters <= 1024, frame_size, n_mfcc, sampling_rate >= 1;
+ * WK_ERR_INVALID_ARG outside it. */
+typedef struct wk_esp_mfcc wk_esp_mfcc;
+wk_status wk_esp_mfcc_create(int32_t sampling_rate, int32_t frame_size, int32_t n_fft, int32_t n_filters,
+                             int32_t n_mfcc, int32_t esp_dsp_packing, int32_t device, wk_esp_mfcc** out);
+wk_status wk_esp_mfcc_run(wk_esp_mfcc* m, const float* d_signal, int64_t batch, int32_t signal_len, int64_t stride,
+                          int32_t hop_size, float pre_emphasis, float* d_out, void* stream);
+wk_status wk_esp_mfcc_destroy(wk_esp_mfcc* m);
+
 /* ---- mfcc.h compatibility shims (main/esp_mfcc/mfcc.h:10-17) --------------
  * Same signatures and ownership as the reference: host signal in, a malloc'd
  * host block of n_frames*n_mfcc floats (frame-major) out, caller frees it with
- * free_mfcc(); NULL on bad arguments.  Computed by the mode-A HIP kernel on
- * device 0 (esp_dsp_packing on).  Only the reference's own configuration
- * (16000 Hz, 320/256/512, 40 filters, 13 coefficients) is supported; other
- * parameters return NULL. */
+ * free_mfcc(); NULL on bad arguments.  Computed on device 0 with
+ * esp_dsp_packing on: the reference configuration (16000 Hz, 320/256/512, 40
+ * filters, 13 coefficients) by the fixed-geometry mode-A kernel, every other
+ * parameter set in wk_esp_mfcc's domain by wk_esp_mfcc (tables cached per
+ * parameter set); NULL outside that domain (non-power-of-2 n_fft, hop_size
+ * < 1, ...). */
 float* extract_mfcc(const float* signal, int signal_len, int sampling_rate, int frame_size, int hop_size,
                     int n_fft, int n_filters, int n_mfcc);
 void free_mfcc(float* mfcc);
 void analyze_mfcc_range(float* mfcc, int size, const char* label);
-/* mfcc.c:297-427 (defined there, not declared in mfcc.h): one 320-sample
- * frame, no pre-emphasis -> malloc'd n_mfcc (<= 13) floats, NULL on error. */
+/* mfcc.c:297-427 (defined there, not declared in mfcc.h): one frame of
+ * frame_size <= n_fft samples, no pre-emphasis -> malloc'd n_mfcc floats, NULL
+ * on error. */
 float* flow_extract_mfcc_single_frame(const float* frame, int frame_size, int sampling_rate, int n_fft, int n_filters,
                                       int n_mfcc);
 

@@ -87,9 +87,11 @@ int esp_mfcc_oracle_fbank(int sr, int n_filters, int n_fft, float* fb) {
  * flow_extract_mfcc_single_frame (mfcc.c:297-427, which has none). */
 int esp_mfcc_oracle_ex(const float* x, int L, int sr, int frame, int hop, int n_fft, int n_filters, int n_mfcc,
                        int esp_pack, float pre, float* out) {
-  if (!x || !out || L < frame || frame <= 0 || hop <= 0 || n_fft < frame || n_filters <= 0 || n_mfcc <= 0 ||
-      n_mfcc > n_filters)
-    return -1;
+  if (!x || !out || L < frame || frame <= 0 || hop <= 0 || n_fft <= 0 || n_filters <= 0 || n_mfcc <= 0) return -1;
+  /* compute_power_spectrum (mfcc.c:252) copies only the first n_fft samples of
+   * a longer frame; dct_ii fills n_filters coefficients and extract_mfcc's
+   * calloc leaves any further ones 0 (mfcc.c:514-517) */
+  const int fl = frame < n_fft ? frame : n_fft;
   const int nf = (L - frame) / hop + 1, nb = n_fft / 2 + 1;
   float* y = (float*)malloc(sizeof(float) * L);
   float* win = (float*)malloc(sizeof(float) * frame);
@@ -118,7 +120,7 @@ int esp_mfcc_oracle_ex(const float* x, int L, int sr, int frame, int hop, int n_
     for (int j = 0; j < frame; ++j) fr[j] = y[t * hop + j] * win[j];
     for (int k = 0; k < nb; ++k) {
       double re = 0.0, im = 0.0;
-      for (int j = 0; j < frame; ++j) {
+      for (int j = 0; j < fl; ++j) {
         const int e = (int)(((long long)j * k) % n_fft);
         re += fr[j] * cs[e];
         im -= fr[j] * sn[e];
@@ -137,6 +139,10 @@ int esp_mfcc_oracle_ex(const float* x, int L, int sr, int frame, int hop, int n_
     }
     for (int c = 0; c < n_mfcc; ++c) {
       float s = 0.0f;
+      if (c >= n_filters) {
+        out[t * n_mfcc + c] = 0.0f;
+        continue;
+      }
       for (int i = 0; i < n_filters; ++i) s += mel[i] * ct[c * n_filters + i];
       out[t * n_mfcc + c] = (c == 0 ? sqrtf(1.0f / n_filters) : sqrtf(2.0f / n_filters)) * s;
     }

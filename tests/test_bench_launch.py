@@ -58,3 +58,79 @@ def test_world_size_must_match_gpus(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
     with pytest.raises(SystemExit, match="WORLD_SIZE=2"):
         bench.main()
+
+
+class _FakeCuda:
+    def __init__(self, n):
+        self.n, self.current = n, None
+
+    def device_count(self):
+        return self.n
+
+    def set_device(self, d):
+        self.current = d
+
+
+class _FakeTorch:
+    def __init__(self, n):
+        self.cuda = _FakeCuda(n)
+
+    @staticmethod
+    def device(s):
+        return ("device", s)
+
+
+class _FakeDist:
+    def __init__(self):
+        self.calls = []
+
+    def init_process_group(self, backend, **kw):
+        self.calls.append((backend, kw))
+
+
+def _args(gpus, backend):
+    import argparse
+    return argparse.Namespace(gpus=gpus, dist_backend=backend)
+
+
+def test_init_rank_nccl_binds_each_rank_to_its_device():
+    """The RCCL branch: each rank of 4 gets its own GPU as device_id."""
+    for r in range(4):
+        env = {"WORLD_SIZE": "4", "RANK": str(r), "LOCAL_RANK": str(r)}
+        t, d = _FakeTorch(8), _FakeDist()
+        world, rank, local, shared = bench.init_rank(_args(4, "nccl"), env, t, d)
+        assert (world, rank, local, shared) == (4, r, r, False)
+        assert t.cuda.current == r
+        assert d.calls == [("nccl", {"device_id": ("device", f"cuda:{r}")})]
+        assert env["MASTER_ADDR"] == "127.0.0.1"
+
+
+def test_init_rank_nccl_refuses_missing_gpu():
+    import pytest
+    env = {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"}
+    with pytest.raises(SystemExit, match="only 1 GPU"):
+        bench.init_rank(_args(2, "nccl"), env, _FakeTorch(1), _FakeDist())
+
+
+def test_init_rank_gloo_rehearsal_is_marked_shared():
+    """Two gloo ranks on one GPU: both use device 0 and the line is a rehearsal."""
+    for r in range(2):
+        env = {"WORLD_SIZE": "2", "RANK": str(r), "LOCAL_RANK": str(r)}
+        t, d = _FakeTorch(1), _FakeDist()
+        world, rank, local, shared = bench.init_rank(_args(2, "gloo"), env, t, d)
+        assert (world, local, shared) == (2, 0, True)
+        assert d.calls == [("gloo", {})]
+
+
+def test_single_rank_forms_no_group():
+    env = {}
+    t, d = _FakeTorch(1), _FakeDist()
+    assert bench.init_rank(_args(1, "nccl"), env, t, d) == (1, 0, 0, False)
+    assert d.calls == []
+
+
+def test_host_threads_reports_affinity():
+    threads, affinity, quota = bench.host_threads()
+    assert affinity == len(os.sched_getaffinity(0))
+    assert 1 <= threads <= affinity
+    assert quota is None or threads <= quota

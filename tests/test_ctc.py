@@ -354,3 +354,71 @@ def test_ctc_fp16_fused_projection_matches_gemm_path(B, monkeypatch):
     assert (lp_f.argmax(-1) == ref_lp.argmax(-1))[ok].all()
     # fp32 gate pre-activations: the fused path is at least as close to the oracle
     assert np.abs((lp_f - ref_lp).numpy()).mean() <= np.abs((lp_g - ref_lp).numpy()).mean() * 1.05
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision,rows", [("fp32", "zero"), ("fp16", "zero"), ("fp16", "equal")])
+@pytest.mark.parametrize("level", [-1.0, 1.0])
+def test_ctc_argmax_ties_keep_first_index(precision, rows, level):
+    """torch.argmax (ctc.py:454) keeps the FIRST of equal maxima.  Output rows
+    40 and 300 get the same bias, on top at a negative (level -1) or positive
+    (+1) level, and either zero weights (every logit is then its bias exactly,
+    whatever the GEMM's order: both paths) or identical weight rows (the fp16
+    output kernel computes both columns with the same instruction sequence, so
+    their logits are bit-identical).  Every frame's argmax must be 40: the
+    fp16 path's column-tagged epilogue as the fp32 path's compare-and-select
+    (advisor finding, round 3: negative ties went to the later column)."""
+    import wakeword
+    m = CO.make_model(V, seed=3)
+    with torch.no_grad():
+        w, b = m.output_layer.weight, m.output_layer.bias
+        if rows == "zero":
+            w.zero_()
+        else:
+            w.mul_(0.01)
+            w[300] = w[40]
+        b.fill_(level - 4.0)
+        b[40] = level
+        b[300] = level
+    g = wakeword.CTCModel(CO.flat_weights(m), V, precision=precision)
+    x = torch.from_numpy(O.synth_clips(8, 0, 6, 48000))
+    feats = CO.features(x)
+    with torch.no_grad():
+        ref = m(feats)
+    # the oracle: rows 40 and 300 on top and equal (up to the CPU GEMM's own order)
+    assert (ref.topk(2, -1).indices.sort(-1).values == torch.tensor([40, 300])).all()
+    assert float((ref[..., 40] - ref[..., 300]).abs().max()) < 1e-5
+    if rows == "zero":
+        assert (ref.argmax(-1) == 40).all()
+    seqs = g.forward(feats)
+    fa = g.frame_argmax(6, feats.shape[1]).cpu()
+    assert (fa == 40).all(), torch.unique(fa)
+    assert seqs == [[40]] * 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["silent", "dc", "dc_and_silent"])
+def test_ctc_transcribe_constant_inputs(ctc, kind):
+    """Constant audio through the one-call path (the z-score folded into the
+    encoder, statistics from the log-mel partials, with the exact two-pass
+    fallback for a variance within the partials' rounding) against the
+    two-call path (features() z-scored by its own two-pass kernel, ctc.py:101-104):
+    digital silence (std 0: left un-normalised), a DC offset (non-silent, the
+    log-mel far from constant) and a batch mixing the two; T = 51."""
+    import wakeword
+    m, _ = ctc
+    g = wakeword.CTCModel(CO.flat_weights(m), V, precision="fp16")
+    n = 8000
+    B, T = 4, 1 + n // 160
+    x = np.zeros((B, n), np.float32)
+    if kind == "dc":
+        x[:] = 0.25
+    elif kind == "dc_and_silent":
+        x[0::2] = 0.25
+    tok, ln = g.decode_audio(x, n_samples=n)
+    one = g.frame_argmax(B, T).cpu()
+    feats = g.features(x, n_samples=n)
+    g.decode(feats)
+    two = g.frame_argmax(B, T).cpu()
+    assert torch.equal(one, two)
+    assert int(ln.min()) >= 0 and int(ln.max()) <= T
