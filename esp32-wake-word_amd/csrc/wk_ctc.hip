@@ -578,23 +578,30 @@ __device__ __forceinline__ float sum_rows4(float v) {
 // registers between the two reductions and the write-back, so the utterance
 // is read from HBM once (it was read three times: 0.27 ms per 4096
 // utterances); longer utterances (> 32,768 values, T > 409) re-read.
+// The sums are double: a constant utterance (digital silence: every value
+// ln(1e-8)) then has mean = its value and std = 0 exactly, and stays
+// un-normalised.  (torch's float std of a constant tensor is rounding noise
+// -- 1.9e-6 for 301 x 80 values of ln(1e-8) -- so ctc.py's `std() > 0` passes
+// and its output is that noise's quotient; the build takes the exact reading,
+// as ctc_zstats_kernel does on the one-call path.)
 constexpr int kZsCache = 8;
 __global__ __launch_bounds__(1024) void ctc_zscore_kernel(float* __restrict__ feats, int64_t n_per) {
-  __shared__ float red[16];
-  __shared__ float bc;
+  __shared__ double red[16];
+  __shared__ double bc;
   float* f = feats + (int64_t)blockIdx.x * n_per;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  auto block_sum = [&](float v) -> float {
-    v = wave_sum(v);
+  auto block_sum = [&](double v) -> double {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) red[w] = v;
     __syncthreads();
     if (tid == 0) {
-      float s = 0.0f;
+      double s = 0.0;
       for (int i = 0; i < 16; ++i) s += red[i];
       bc = s;
     }
     __syncthreads();
-    const float r = bc;
+    const double r = bc;
     __syncthreads();
     return r;
   };
@@ -602,48 +609,44 @@ __global__ __launch_bounds__(1024) void ctc_zscore_kernel(float* __restrict__ fe
   if (n_per % 4 == 0 && n4 <= 1024 * kZsCache && ((uintptr_t)f & 15) == 0) {
     float4* f4 = reinterpret_cast<float4*>(f);
     float4 v[kZsCache];
-    float s = 0.0f;
+    double s = 0.0;
 #pragma unroll
     for (int k = 0; k < kZsCache; ++k) {
       const int64_t i = tid + 1024 * k;
       v[k] = i < n4 ? f4[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+      s += ((double)v[k].x + (double)v[k].y) + ((double)v[k].z + (double)v[k].w);
     }
-    const float mean = block_sum(s) / (float)n_per;
-    float q = 0.0f;
+    const double mean = block_sum(s) / (double)n_per;
+    double q = 0.0;
 #pragma unroll
     for (int k = 0; k < kZsCache; ++k) {
       if (tid + 1024 * k < n4) {
-        const float a = v[k].x - mean, b = v[k].y - mean, c = v[k].z - mean, d = v[k].w - mean;
-        q = __builtin_fmaf(a, a, q);
-        q = __builtin_fmaf(b, b, q);
-        q = __builtin_fmaf(c, c, q);
-        q = __builtin_fmaf(d, d, q);
+        const double a = v[k].x - mean, b = v[k].y - mean, c = v[k].z - mean, d = v[k].w - mean;
+        q += (a * a + b * b) + (c * c + d * d);
       }
     }
-    const float sd = sqrtf(block_sum(q) / (float)(n_per - 1));
-    if (!(sd > 0.0f)) return;   // ctc.py:101-104: only when std > 0
-    const float inv = 1.0f / sd;
+    const double sd = sqrt(block_sum(q) / (double)(n_per - 1));
+    if (!(sd > 0.0)) return;   // ctc.py:101-104: only when std > 0
+    const float mf = (float)mean, inv = (float)(1.0 / sd);
 #pragma unroll
     for (int k = 0; k < kZsCache; ++k) {
       const int64_t i = tid + 1024 * k;
-      if (i < n4)
-        f4[i] = make_float4((v[k].x - mean) * inv, (v[k].y - mean) * inv, (v[k].z - mean) * inv, (v[k].w - mean) * inv);
+      if (i < n4) f4[i] = make_float4((v[k].x - mf) * inv, (v[k].y - mf) * inv, (v[k].z - mf) * inv, (v[k].w - mf) * inv);
     }
     return;
   }
-  float s = 0.0f;
-  for (int64_t i = tid; i < n_per; i += 1024) s += f[i];
-  const float mean = block_sum(s) / (float)n_per;
-  float q = 0.0f;
+  double s = 0.0;
+  for (int64_t i = tid; i < n_per; i += 1024) s += (double)f[i];
+  const double mean = block_sum(s) / (double)n_per;
+  double q = 0.0;
   for (int64_t i = tid; i < n_per; i += 1024) {
-    const float d = f[i] - mean;
-    q = __builtin_fmaf(d, d, q);
+    const double d = (double)f[i] - mean;
+    q += d * d;
   }
-  const float sd = sqrtf(block_sum(q) / (float)(n_per - 1));
-  if (!(sd > 0.0f)) return;
-  const float inv = 1.0f / sd;
-  for (int64_t i = tid; i < n_per; i += 1024) f[i] = (f[i] - mean) * inv;
+  const double sd = sqrt(block_sum(q) / (double)(n_per - 1));
+  if (!(sd > 0.0)) return;
+  const float mf = (float)mean, inv = (float)(1.0 / sd);
+  for (int64_t i = tid; i < n_per; i += 1024) f[i] = (f[i] - mf) * inv;
 }
 
 // The z-score's statistics for wk_ctc_transcribe: one wave per utterance

@@ -98,16 +98,18 @@ def _declare(L):
     L.wk_augment.argtypes = [vp, i32, C.c_float, C.c_float, C.c_float, u32, vp, i32]
     L.wk_device_cmvn.argtypes = [vp, i32, i64, vp, vp, vp]
     L.wk_check_device_errors.argtypes = [vp, C.POINTER(u32)]
-    L.wk_esp_mfcc_create.argtypes = [i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp)]
-    L.wk_esp_mfcc_run.argtypes = [vp, vp, i64, i32, i64, i32, C.c_float, vp, vp]
-    L.wk_esp_mfcc_destroy.argtypes = [vp]
+    if hasattr(L, "wk_esp_mfcc_create"):   # (absent from pre-round-4 libraries loaded for A/B timing)
+        L.wk_esp_mfcc_create.argtypes = [i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp)]
+        L.wk_esp_mfcc_run.argtypes = [vp, vp, i64, i32, i64, i32, C.c_float, vp, vp]
+        L.wk_esp_mfcc_destroy.argtypes = [vp]
     for name in ("wk_create", "wk_destroy", "wk_mfcc", "wk_cnn", "wk_forward", "wk_synth_clips", "wk_normalize",
                  "wk_stream_create", "wk_stream_destroy", "wk_stream_reset", "wk_stream_push", "wk_ctc_create",
                  "wk_ctc_destroy", "wk_ctc_features", "wk_ctc_forward", "wk_wav_read", "wk_wav_load_batch",
                  "wk_augment", "wk_device_cmvn", "wk_ctc_frame_argmax", "wk_record_front",
                  "wk_quantize_frames", "wk_ctc_profile", "wk_ctc_stage_times", "wk_ctc_transcribe",
                  "wk_esp_mfcc_create", "wk_esp_mfcc_run", "wk_esp_mfcc_destroy"):
-        getattr(L, name).restype = i32
+        if hasattr(L, name):
+            getattr(L, name).restype = i32
 
 
 def lib():

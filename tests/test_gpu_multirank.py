@@ -39,11 +39,13 @@ def test_two_ranks_shard_equals_unsharded(tmp_path, precision):
 @pytest.mark.gpu
 def test_bench_self_launch_reports_world(tmp_path):
     """`bench.py --gpus 2` spawns two ranks itself (gloo here: they share the GPU);
-    rank 0's line carries n_gpus = 2 and the process-group world it observed."""
+    rank 0's line carries n_gpus = 2 and the process-group world it observed,
+    and, the ranks sharing one GPU, is marked a rehearsal with no throughput."""
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "2",
            "--warmup", "1", "--batch", "8192", "--no-cpu-baseline"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["config"]["process_group_world_size"] == 2
-    assert line["config"]["global_batch"] == 2 * 8192 and line["value"] > 0
+    assert line["config"]["global_batch"] == 2 * 8192 and line["rehearsal"] is True
+    assert line["value"] is None and line["roofline"]["frac"] is None and line["ms_per_step"] > 0
