@@ -30,7 +30,7 @@ struct wk_handle {
   uint16_t* d_bf16;      // bf16 conv fragments (WK_PREC_BF16; BF16X3: hi then lo, wk::pack_fragments_bf16)
   int64_t ws_clips;
   int unfused;           // WAKEWORD_UNFUSED=1: front-end + CNN as two kernels (A/B testing)
-  int fused_exp;         // WAKEWORD_FUSED_EXP, -DWK_DEBUG_EXPERIMENTS builds only: role-isolation timing
+  int fused_exp;         // WAKEWORD_FUSED_EXP, -DWK_DIAG builds only: role-isolation timing
                          // experiments (wrong logits); always 0 in the shipped library
 };
 
@@ -101,7 +101,7 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
   {
     const char* u = getenv("WAKEWORD_UNFUSED");
     h->unfused = u && u[0] == '1';
-#ifdef WK_DEBUG_EXPERIMENTS
+#ifdef WK_DIAG
     const char* fx = getenv("WAKEWORD_FUSED_EXP");
     h->fused_exp = fx ? atoi(fx) : 0;
 #endif

@@ -11,19 +11,6 @@
 #pragma once
 #include "wk_common.h"
 
-#ifdef WK_EPI_CHECK
-// Diagnostic build only: bf16 epilogue stores outside their image / pooled
-// buffer are counted, and the first one's (kind, lane, co0, clip, t0, index).
-__device__ unsigned g_epi_bad[8];
-__device__ __forceinline__ void epi_check(int kind, long idx, long lim, int lane, int co0, int clip, int t0) {
-  if (idx < 0 || idx >= lim) {
-    if (atomicAdd(&g_epi_bad[0], 1u) == 0u) {
-      g_epi_bad[1] = kind; g_epi_bad[2] = lane; g_epi_bad[3] = co0; g_epi_bad[4] = clip; g_epi_bad[5] = t0;
-      g_epi_bad[6] = (unsigned)idx; g_epi_bad[7] = (unsigned)lim;
-    }
-  }
-}
-#endif
 
 namespace wk {
 
@@ -51,12 +38,7 @@ __device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g,
     s += dpp<0x4E>(s);
     s += dpp<0x141>(s);
     s += dpp<0x140>(s);
-#if !defined(WK_ABL_NOEPI) && !defined(WK_ABL_NOGAPST)
-#ifdef WK_EPI_CHECK
-    if (tt == 0) epi_check(1, (long)(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip, 128L * GSTRIDE, lane, co0, clip, r);
-#endif
     if (tt == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s / 7.0f;
-#endif
   }
 }
 
@@ -64,41 +46,22 @@ __device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g,
 // Fragments hold 8 bf16 per lane (K = 32 per step): one 16-byte LDS read per
 // B fragment and one 16-byte load per A fragment.  A step is issued as two
 // CDNA3-era v_mfma_f32_16x16x16_bf16 (elements 0-3, then 4-7 of each lane).
-// gfx950's single-instruction K=32 form (v_mfma_f32_16x16x32_bf16, -DWK_MFMA_K32)
-// is the same work in the same ~16 cycles as ONE K=16 instruction
-// (tools/debug/mfma_rate.hip), but in this kernel it corrupts the front-end
-// (tools/debug/k32_probe.py): the front-end's own
-// log-mel image of 10-30 % of the clips changes run to run -- a few adjacent
-// mel rows of one frame in 48-62, i.e. a few power bins written by lanes 48-63
-// of a front-end wave -- and the DCT reads exactly what the front-end left
-// (the hand-off protocol is not involved).  It needs the CNN role's epilogue
-// LDS stores (with the pool stores or the GAP stores alone it persists, with
-// neither it is gone), every one of which is in bounds (checked), and it
-// survives 8 wait states after every K=32 MFMA with nothing scheduled across
-// them.  The K=16 pair is bit-repeatable.  So the K=32 form is rejected: the
-// build refuses it unless WK_ALLOW_K32_DIAG (diagnostic variants only).
+// gfx950's single-instruction K=32 form (v_mfma_f32_16x16x32_bf16) is the
+// same work in the same ~16 cycles as ONE K=16 instruction, but with it the
+// fused kernel's front-end log-mel images changed run to run (round 3,
+// DESIGN.md 5.1): the cause was not found, so the form is not used.  What
+// bounds the K=16 pair's exposure to the same unknown: the CNN carve is
+// disjoint from the front-end's power rows and log-mel buffers
+// (static_asserts in wk_fused.hip), and four full-size launches per precision
+// are compared bit for bit (tests/test_gpu_bf16.py::test_fused_repeatable_at_scale).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s8 __attribute__((ext_vector_type(8)));   // one lane's A or B fragment: 8 bf16 bit patterns
 
-#if defined(WK_MFMA_K32) && !defined(WK_ALLOW_K32_DIAG)
-#error "WK_MFMA_K32 corrupts the fused kernel's front-end (see above); diagnostic builds add -DWK_ALLOW_K32_DIAG"
-#endif
 __device__ __forceinline__ f32x4 mfma_bf16(s8 a, s8 b, f32x4 c) {
-#ifdef WK_MFMA_K32
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
-                                              0);
-#ifdef WK_K32_PAD   // diagnostic: >= 8 wait states after every K=32 MFMA, nothing scheduled across them
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7");
-  __builtin_amdgcn_sched_barrier(0);
-#endif
-  return c;
-#else
   c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 0, 1, 2, 3),
                                                 __builtin_shufflevector(b, b, 0, 1, 2, 3), c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 4, 5, 6, 7),
                                                    __builtin_shufflevector(b, b, 4, 5, 6, 7), c, 0, 0, 0);
-#endif
 }
 
 __device__ __forceinline__ uint32_t bf16_bits(float x) {   // round to nearest even
@@ -152,13 +115,6 @@ __device__ __forceinline__ void epi_pool_bf(const f32x4& acc, uint16_t* __restri
     const float x = fmaxf(acc[r], 0.0f);
     v[r] = fmaxf(x, swap_adjacent(x));
   }
-#if defined(WK_ABL_NOEPI) || defined(WK_ABL_NOPOOLST)   // diagnostic: bf16 conv epilogues store nothing (results wrong)
-  if (lane >= 0) return;
-#endif
-#ifdef WK_EPI_CHECK
-  if (!(lane & 1) && tp < TN)
-    epi_check(2, (long)(clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4), 4L * TP_N * CIP_N, lane, co0, clip, t0);
-#endif
   if (!(lane & 1) && tp < TN) {
     uint2 pkd;
     pkd.x = bf16_bits(v[0]) | (bf16_bits(v[1]) << 16);

@@ -158,10 +158,10 @@ template <> __device__ __forceinline__ float sample<int16_t>(const int16_t* p, i
   return (float)p[i] * (1.0f / 32768.0f);
 }
 
-// Diagnostic builds only (-DWK_STAMPS, tools/debug): per-phase s_memtime
+// Diagnostic builds only (-DWK_DIAG, tools/debug): per-phase s_memtime
 // cycle sums.  Device helpers take an optional WkStamps* (WK_SP_PARAM) and
 // mark phase ends with WK_FE_HIT(k); product builds compile all of it away.
-#ifdef WK_STAMPS
+#ifdef WK_DIAG
 struct WkStamps {
   unsigned long long st[16];
   unsigned long long tl;
@@ -177,9 +177,6 @@ struct WkStamps {
 };
 #define WK_SP_PARAM , WkStamps* stp = nullptr
 #define WK_FE_HIT(k) do { if (stp) stp->hit(k); } while (0)
-#elif defined(WK_ASM_MARKS)   // dev builds: phase markers in the -S output (tools/asm_phases.py)
-#define WK_SP_PARAM
-#define WK_FE_HIT(k) asm volatile(";WKMARK fe" #k)
 #else
 #define WK_SP_PARAM
 #define WK_FE_HIT(k) do {} while (0)

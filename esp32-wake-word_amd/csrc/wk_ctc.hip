@@ -7,9 +7,11 @@
 //         -> greedy CTC decode (ctc.py:453-471)
 //
 // Kernels:
-//   ctc_logmel_fft_kernel reflect-padded frames x periodic Hann(400) -> 400-point
-//                         real DFT as a 20 x 20 four-step FFT in registers + LDS
-//                         -> power -> HTK mel (CSR weights) -> ln(+1e-8), fused.
+//   ctc_logmel_fft2_kernel reflect-padded frames x periodic Hann(400) -> 400-point
+//                         real DFT (two frames per complex 20 x 20 four-step FFT)
+//                         -> power -> HTK mel -> ln(+1e-8), fused; optionally the
+//                         z-score's per-pass partial sums.
+//   ctc_zstats_kernel     {mean, 1/std} per utterance from those partials.
 //   ctc_zscore_kernel     one block per utterance, two-pass mean / unbiased std.
 //   ctc_encoder_kernel    Linear 80->128 as fp32 MFMA tiles of 16 rows, LayerNorm
 //                         by in-register + 16-lane shuffle sums.
@@ -49,45 +51,10 @@ namespace {
 constexpr int kNfft = 400, kHop = 160, kBins = kNfft / 2 + 1, kMels = 80, kH = 128;
 
 // ---------------------------------------------------------------------------
-// X1: log-mel
+// X1: log-mel.  The 400-point DFT is 20 x 20 four-step (n = 20 n1 + n2,
+// k = k1 + 20 k2), each DFT-20 4 x DFT-5 + constant twiddles + 5 x DFT-4 in
+// packed fp32 (ctc_logmel_fft2_kernel below).
 // ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-// X1 as one kernel: frames -> 400-point real DFT by FFT -> power -> HTK mel ->
-// ln(+1e-8).  The DFT is 400 = 20 x 20 four-step (n = 20 n1 + n2,
-// k = k1 + 20 k2): stage 1, lane (frame, n2) takes its 20 real samples
-// x[20 n1 + n2] (reflect-padded, Hann-windowed) through an in-register DFT-20
-// over n1 -> A[n2][k1] (k1 = 0..10 kept: real input, A[n2][20-k1] = conj);
-// stage 2, lane (frame, k1), k1 = 0..19, gathers A[.][k1] through LDS (conj of
-// A[.][20-k1] for k1 > 10), twiddles by W400^(n2 k1) (LDS table) and runs a
-// DFT-20 over n2 -> X[k1 + 20 k2].  Each DFT-20 is 4 x DFT-5 + constant
-// twiddles + 5 x DFT-4, packed fp32.  Three frames per wave (60 lanes), one
-// LDS region per wave, no block barrier in the loop.  ~4.6 kflop per frame
-// instead of the 321 kflop of the DFT-as-GEMM it replaces.
-// ---------------------------------------------------------------------------
-constexpr int kFftWaves = 4, kFftFrames = 3;           // frames per wave pass
-// LDS pitches (float2 / float units) chosen so that every wave-wide access is
-// bank-conflict-free for the 3-frame lane layout (lanes 0-19, 20-39, 40-59):
-// A rows of 15 float2 (stage-1 ds_write_b64 and stage-2 ds_read_b64 both), twiddle
-// rows of 21 float2 (stage-2 reads, lane = k1), power rows of 212 floats (212 = 20
-// mod 64: the three frames' 20-lane writes fill disjoint bank ranges).  With 11 /
-// 20 / 204, 45 % of the kernel's LDS cycles were conflicts (PMC).
-constexpr int kAPitch = 15;                             // A[f][n2][k1], k1 = 0..10 (float2)
-constexpr int kTwPitch = 21;
-constexpr int kPwPitch = 212;
-constexpr int kFbMaxW = 640;                           // CSR mel weights kept in LDS (host checks nnz)
-struct CtcFftLds {
-  float fbw[kFbMaxW];
-  int fbs[kMels], fbl[kMels], fbo[kMels];
-  float win[kNfft];
-  f2 tw[20][kTwPitch];                                  // W400^(n2 k1), [k1][n2]
-  // per wave: the stage-1 -> stage-2 matrix, and the power rows written by
-  // stage 2 after its last read of it (one wave's LDS ops complete in order)
-  union {
-    f2 a[kFftFrames * 20 * kAPitch];
-    float pw[kFftFrames][kPwPitch];
-  } w[kFftWaves];
-};
-
 // W20^e = exp(-2 pi i e / 20).
 __constant__ constexpr float kW20c[20] = {1.000000000e+00f, 9.510565163e-01f, 8.090169944e-01f, 5.877852523e-01f, 3.090169944e-01f, 0.000000000e+00f, -3.090169944e-01f, -5.877852523e-01f, -8.090169944e-01f, -9.510565163e-01f, -1.000000000e+00f, -9.510565163e-01f, -8.090169944e-01f, -5.877852523e-01f, -3.090169944e-01f, 0.000000000e+00f, 3.090169944e-01f, 5.877852523e-01f, 8.090169944e-01f, 9.510565163e-01f};
 __constant__ constexpr float kW20s[20] = {0.000000000e+00f, -3.090169944e-01f, -5.877852523e-01f, -8.090169944e-01f, -9.510565163e-01f, -1.000000000e+00f, -9.510565163e-01f, -8.090169944e-01f, -5.877852523e-01f, -3.090169944e-01f, 0.000000000e+00f, 3.090169944e-01f, 5.877852523e-01f, 8.090169944e-01f, 9.510565163e-01f, 1.000000000e+00f, 9.510565163e-01f, 8.090169944e-01f, 5.877852523e-01f, 3.090169944e-01f};
@@ -133,125 +100,6 @@ __device__ __forceinline__ void dft20(f2 (&x)[20]) {
   for (int k = 0; k < 20; ++k) x[k] = y[k];
 }
 
-__global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __restrict__ audio, int64_t stride,
-                                                             int n_valid, int n_pad, int T, int64_t rows,
-                                                             const float* __restrict__ win_g,
-                                                             const float* __restrict__ tw_g,
-                                                             const int* __restrict__ fb_start,
-                                                             const int* __restrict__ fb_len,
-                                                             const int* __restrict__ fb_off,
-                                                             const float* __restrict__ fb_w, int n_fbw,
-                                                             float* __restrict__ feats) {
-  __shared__ CtcFftLds L;
-  for (int i = threadIdx.x; i < kNfft; i += 256) L.win[i] = win_g[i];
-  for (int i = threadIdx.x; i < 400; i += 256) L.tw[i / 20][i % 20] = f2{tw_g[2 * i], tw_g[2 * i + 1]};
-  for (int i = threadIdx.x; i < kMels; i += 256) {
-    L.fbs[i] = fb_start[i];
-    L.fbl[i] = fb_len[i];
-    L.fbo[i] = fb_off[i];
-  }
-  for (int i = threadIdx.x; i < n_fbw; i += 256) L.fbw[i] = fb_w[i];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int f = lane / 20, q = lane - 20 * (lane / 20);   // frame slot (3 = idle lanes 60-63), n2 / k1
-  f2* A = L.w[wv].a;
-  float* PW = &L.w[wv].pw[0][0];
-  const int64_t passes = (rows + kFftFrames - 1) / kFftFrames;
-  const int64_t pstep = (int64_t)gridDim.x * kFftWaves;
-  // The lane's 20 samples x[20 n1 + q] of pass ps_'s frame f: the next pass's
-  // are loaded while this pass's FFTs and mel run.  Both paths are wave-uniform
-  // and issue exactly 20 loads with no per-lane branch, so the compiler's load
-  // counter stays exact across the loop (a per-lane branch made it wait for the
-  // prefetch before stage 1).  Idle lanes read the first samples of utterance 0
-  // on the interior path; nothing they compute is stored.
-  const int nv_min = n_valid < n_pad ? n_valid : n_pad;
-  auto load_raw = [&](int64_t ps_, float (&raw)[20]) {
-    const int64_t row = ps_ * kFftFrames + f;
-    const bool live = f < kFftFrames && ps_ < passes && row < rows;
-    const int rr = live ? (int)row : 0;   // rows < 2^31 (host check)
-    const int b = (int)((unsigned)rr / (unsigned)T), t = rr - b * T;
-    const float* xa = audio + (int64_t)b * stride;
-    const int p0 = live ? t * kHop - kNfft / 2 : 0;
-    if (__all(p0 >= 0 && p0 + kNfft <= nv_min)) {
-      // interior frames inside the valid samples (all but ~2 frames per
-      // utterance): no reflection, no padding -- 20 loads off one address
-      const float* xp = xa + p0 + q;
-#pragma unroll
-      for (int n1 = 0; n1 < 20; ++n1) raw[n1] = xp[20 * n1];
-    } else {
-#pragma unroll
-      for (int n1 = 0; n1 < 20; ++n1) {
-        int p = p0 + 20 * n1 + q;
-        p = p < 0 ? -p : p;
-        p = p > n_pad - 1 ? 2 * (n_pad - 1) - p : p;
-        const bool in = p < n_valid;
-        const float x = xa[in ? p : 0];
-        raw[n1] = in ? x : 0.0f;
-      }
-    }
-  };
-  float raw[20];
-  load_raw((int64_t)blockIdx.x * kFftWaves + wv, raw);
-  for (int64_t ps = (int64_t)blockIdx.x * kFftWaves + wv; ps < passes; ps += pstep) {
-    const int64_t row = ps * kFftFrames + f;
-    const bool act = f < kFftFrames && row < rows;
-    // stage 1: lane (f, n2 = q): DFT-20 over n1 of x[20 n1 + n2]
-    f2 v[20];
-#pragma unroll
-    for (int n1 = 0; n1 < 20; ++n1) {
-      v[n1] = f2{raw[n1] * L.win[20 * n1 + q], 0.0f};
-      // pin the product here, ahead of the next pass's loads: otherwise it sinks
-      // into the stage-1 block, the old and new samples are live together and
-      // the loop-carried copies make every pass wait for its own prefetch
-      asm volatile("" ::"v"(v[n1].x) : "memory");
-    }
-    load_raw(ps + pstep, raw);
-    dft20(v);
-    if (act) {
-#pragma unroll
-      for (int k1 = 0; k1 <= 10; ++k1) A[(f * 20 + q) * kAPitch + k1] = v[k1];
-    }
-    wave_lds_sync();
-    // stage 2: lane (f, k1 = q): twiddle + DFT-20 over n2 -> X[k1 + 20 k2]
-    if (act) {
-      const bool mirror = q > 10;
-      const int kc = mirror ? 20 - q : q;
-      const f2 sg = mirror ? f2{1.0f, -1.0f} : f2{1.0f, 1.0f};   // conj for k1 > 10
-      f2 v[20];
-#pragma unroll
-      for (int n2 = 0; n2 < 20; ++n2) v[n2] = cmul2(A[(f * 20 + n2) * kAPitch + kc] * sg, L.tw[q][n2]);
-      dft20(v);
-      float* pw = PW + f * kPwPitch;
-#pragma unroll
-      for (int k2 = 0; k2 < 10; ++k2) pw[q + 20 * k2] = __builtin_fmaf(v[k2].x, v[k2].x, v[k2].y * v[k2].y);
-      if (q == 0) pw[200] = __builtin_fmaf(v[10].x, v[10].x, v[10].y * v[10].y);
-    }
-    wave_lds_sync();
-    // power -> HTK mel (CSR) -> ln(+1e-8): lane = mel, all three frames per
-    // weight (lanes 0-15 also take mel 64 + lane).  A wave walks the widest
-    // filter of each of the two lane sets (~9 + 12 taps) instead of four rounds
-    // of (frame, mel) tasks, each as long as its widest filter (~44 taps).
-    auto mel3 = [&](int m) {
-      const int s0 = L.fbs[m], n = L.fbl[m], o = L.fbo[m];
-      const float* pw = PW + s0;
-      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
-      for (int j = 0; j < n; ++j) {
-        const float wj = L.fbw[o + j];
-        a0 = __builtin_fmaf(pw[j], wj, a0);
-        a1 = __builtin_fmaf(pw[kPwPitch + j], wj, a1);
-        a2 = __builtin_fmaf(pw[2 * kPwPitch + j], wj, a2);
-      }
-      const int64_t r0 = ps * kFftFrames;
-      if (r0 < rows) feats[r0 * kMels + m] = wk_logf(a0 + 1e-8f);
-      if (r0 + 1 < rows) feats[(r0 + 1) * kMels + m] = wk_logf(a1 + 1e-8f);
-      if (r0 + 2 < rows) feats[(r0 + 2) * kMels + m] = wk_logf(a2 + 1e-8f);
-    };
-    static_assert(kFftFrames == 3 && kMels > 64 && kMels <= 128, "mel lane mapping");
-    mel3(lane);
-    if (lane < kMels - 64) mel3(64 + lane);
-    wave_lds_sync();
-  }
-}
 
 // ---------------------------------------------------------------------------
 // X1, two frames per complex FFT (round 3).  The 400-point DFT of a real frame
@@ -278,22 +126,11 @@ __global__ __launch_bounds__(256) void ctc_logmel_fft_kernel(const float* __rest
 // LDS pitches (see the per-access notes) keep the stage-1 writes, stage-2
 // reads and pair-power writes free of bank conflicts.
 // ---------------------------------------------------------------------------
-#ifndef WK_LM_NOPAIR
-#define WK_LM_NOPAIR 1
-#endif
-#ifndef WK_LM_NOREAD2
-#define WK_LM_NOREAD2 1
-#endif
-#ifndef WK_LM_REGTW
-#define WK_LM_REGTW 0   // (measured 0.59 vs 0.48 ms: 2 waves per SIMD lose more than the LDS reads save) 1: window and twiddles of the lane in registers, 8 waves per workgroup (2 per SIMD)
-#endif
-constexpr int kF2Waves = WK_LM_REGTW ? 8 : 12, kF2Pairs = 3;
+constexpr int kF2Waves = 12, kF2Pairs = 3;
+constexpr int kTwPitch = 21;    // twiddle rows (float2): stage-2 reads, lane = k1
 constexpr int kMelW1 = 8, kMelW2 = 7;   // mel windows: mels 0-63 <= 8 bins, mels 64-79 <= 14 = 2 x 7 (host-checked)
 constexpr int kA2Pitch = 25;    // A[g][n2][k1] rows (float2): 25 = 1 mod 8 -> stage-2 lane groups start 40 banks apart
-#ifndef WK_E2_PITCH
-#define WK_E2_PITCH 11
-#endif
-constexpr int kE2Pitch = WK_E2_PITCH;   // exchange rows (float2): 22 dwords -> 20 partner rows on distinct banks
+constexpr int kE2Pitch = 11;   // exchange rows (float2): 22 dwords -> 20 partner rows on distinct banks
                                 // (pitch 12 put them on 8 bank pairs: 24 p mod 64 has period 8)
 constexpr int kP2Pitch = 212;   // pair-power rows (float2): 2 x 212 = 40 mod 64 banks between lane groups
 static_assert(kF2Pairs * kP2Pitch <= kF2Pairs * 20 * kA2Pitch, "power rows alias the A region");
@@ -334,24 +171,10 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (buffer resources)
   const int g = lane / 20, q = lane - 20 * (lane / 20);   // pair slot (3 = idle lanes 60-63), n2 / k1
-  float wreg[WK_LM_REGTW ? 20 : 1];
-  f2 twreg[WK_LM_REGTW ? 20 : 1];
-  if constexpr (WK_LM_REGTW) {
-#pragma unroll
-    for (int j = 0; j < 20; ++j) {
-      wreg[j] = L.win[20 * j + q];
-      twreg[j] = L.tw[q][j];
-    }
-  }
   f2* A = L.w[wv];
-#if WK_LM_NOPAIR   // (A/B) every 8-byte LDS access single: the compiler pairs neighbours into ds_read2/write2_b64
   typedef volatile __attribute__((address_space(3))) f2 vlf2;
 #define LM_R(p, i) (*(const vlf2*)((p) + (i)))
 #define LM_W(p, i, val) (*(vlf2*)((p) + (i)) = (val))
-#else
-#define LM_R(p, i) ((p)[i])
-#define LM_W(p, i, val) ((p)[i] = (val))
-#endif
   constexpr int kRowsPerPass = 2 * kF2Pairs;
   const int64_t passes = (rows + kRowsPerPass - 1) / kRowsPerPass;
   const int64_t pstep = (int64_t)gridDim.x * kF2Waves;
@@ -409,7 +232,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     f2 v[20];
 #pragma unroll
     for (int n1 = 0; n1 < 20; ++n1) {
-      const float wn = WK_LM_REGTW ? wreg[n1] : L.win[20 * n1 + q];
+      const float wn = L.win[20 * n1 + q];
       v[n1] = f2{ra[n1], rb[n1]} * f2{wn, wn};
       asm volatile("" ::"v"(v[n1].x), "v"(v[n1].y) : "memory");   // ahead of the next pass's loads
     }
@@ -426,7 +249,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     // 40 g x 25 = 40 g mod 64 dwords, so half-waves touch disjoint banks
     if (lact) {
 #pragma unroll
-      for (int n2 = 0; n2 < 20; ++n2) v[n2] = cmul2(LM_R(A, (g * 20 + n2) * kA2Pitch + q), WK_LM_REGTW ? twreg[n2] : L.tw[q][n2]);
+      for (int n2 = 0; n2 < 20; ++n2) v[n2] = cmul2(LM_R(A, (g * 20 + n2) * kA2Pitch + q), L.tw[q][n2]);
     }
     dft20(v);   // Z[q + 20 k2] in v[k2]
     // exchange (the A reads of this wave are done: one wave's LDS ops complete in order)
@@ -476,12 +299,8 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
       const f2* p2 = PW + ws2;
       f2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f}, a2 = {0.0f, 0.0f};
       f2 c0 = {0.0f, 0.0f}, c1 = {0.0f, 0.0f}, c2 = {0.0f, 0.0f};
-#if WK_LM_NOREAD2   // (A/B) single 8-byte reads: the compiler would pair them into ds_read2_b64
       typedef const volatile __attribute__((address_space(3))) f2 vf2;
 #define LM_RD(p, i) (*(vf2*)((p) + (i)))
-#else
-#define LM_RD(p, i) ((p)[i])
-#endif
 #pragma unroll
       for (int j = 0; j < kMelW1; ++j) {
         a0 = fma2(LM_RD(p1, j), f2{mw1[j], mw1[j]}, a0);
@@ -800,12 +619,6 @@ typedef _Float16 h8e __attribute__((ext_vector_type(8)));
 // Output rows are time-major (row t B + b for input row b T + t): the fp16
 // path keeps every [rows][.] tensor after the encoder in that order, so that a
 // GRU step's 16 utterances are 16 adjacent rows of the gate inputs and outputs.
-#ifndef WK_GRU_HSINGLE
-#define WK_GRU_HSINGLE 0
-#endif
-#ifndef WK_ENC_PF
-#define WK_ENC_PF 1   // fp16 encoder: 16-row blocks of input in flight per wave
-#endif
 // NORM (wk_ctc_transcribe): the input rows are raw log-mel; each is z-scored
 // with its utterance's zs = {mean, 1/std} (ctc_zstats_kernel) as it is loaded.
 template <bool NORM>
@@ -843,9 +656,9 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
   // waited for everything: ~60 % of wave-cycles were waits, PMC).
   const __amdgpu_buffer_rsrc_t irs = make_rsrc(in, (uint32_t)(rows * kMels * 4));   // < 2^31 B (host check)
   const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, (uint32_t)(rows * kH * 2));
-  // WK_ENC_PF blocks of input rows in flight per wave (a block's compute is
+  // 1 blocks of input rows in flight per wave (a block's compute is
   // far shorter than the HBM latency)
-  float4 xr[WK_ENC_PF][KS][2];
+  float4 xr[1][KS][2];
   auto load_blk = [&](int64_t blk, float4 (&x)[KS][2]) __attribute__((always_inline)) {
     const int64_t r = blk * 16 + li;
 #pragma unroll
@@ -879,7 +692,7 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
                      (_Float16)b.x, (_Float16)b.y, (_Float16)b.z, (_Float16)b.w};
       }
     }
-    load_blk(blk + WK_ENC_PF * G, x);   // the block WK_ENC_PF ahead into this slot (past the end: zeros, unused)
+    load_blk(blk + 1 * G, x);   // the block 1 ahead into this slot (past the end: zeros, unused)
     f32x4 acc[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc[ct] = *reinterpret_cast<const f32x4*>(&pb[0][16 * ct + 4 * lg]);   // + bias
@@ -921,10 +734,10 @@ __global__ __launch_bounds__(256) void ctc_encoder16_kernel(const float* __restr
   };
   int64_t blk = (int64_t)blockIdx.x * 4 + wv;
 #pragma unroll
-  for (int u = 0; u < WK_ENC_PF; ++u) load_blk(blk + u * G, xr[u]);
-  for (; blk < nblk; blk += WK_ENC_PF * G) {
+  for (int u = 0; u < 1; ++u) load_blk(blk + u * G, xr[u]);
+  for (; blk < nblk; blk += 1 * G) {
 #pragma unroll
-    for (int u = 0; u < WK_ENC_PF; ++u) {
+    for (int u = 0; u < 1; ++u) {
       if (blk + u * G >= nblk) break;   // (wave-uniform)
       body(blk + u * G, xr[u]);
     }
@@ -1030,13 +843,7 @@ typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 constexpr int kH16P = kH + 8;   // LDS pitch (halves) of the fp16 state image [batch][unit]: 16-byte rows, conflict-free B reads
 constexpr int kGru16Waves = kH / 16, kGru16Threads = 64 * kGru16Waves;
 constexpr int kGtP = 3 * kH + 8;   // LDS pitch (halves) of a gate-input tile row: 16-byte aligned
-#ifndef WK_GRU_PF
-#define WK_GRU_PF 2
-#endif
-constexpr int kGruPf = WK_GRU_PF;
-#ifndef WK_GRU_ABL
-#define WK_GRU_ABL 0
-#endif   // gate-input prefetch depth (steps)
+constexpr int kGruPf = 2;
 
 __global__ __launch_bounds__(kGru16Threads, 4) void ctc_gru16_kernel(const __half* __restrict__ gi, const h4* __restrict__ whh_pk,
                                                                   const float* __restrict__ bih,
@@ -1112,9 +919,7 @@ __global__ __launch_bounds__(kGru16Threads, 4) void ctc_gru16_kernel(const __hal
   __half* yq = out + ((int64_t)(dir == 0 ? 0 : T - 1) * B + (ylive ? (int64_t)blockIdx.x * kGruBatch + yn : 0)) * (2 * kH) +
                dir * kH + 8 * yc;
   auto store_y = [&](int buf) {
-#if WK_GRU_ABL != 3
     if (ylive) *reinterpret_cast<uint4*>(yq) = *reinterpret_cast<const uint4*>(&h16[buf][yn * kH16P + 8 * yc]);
-#endif
     yq += dstep * (2 * kH);
   };
 #pragma unroll
@@ -1147,9 +952,7 @@ __global__ __launch_bounds__(kGru16Threads, 4) void ctc_gru16_kernel(const __hal
              gc = *reinterpret_cast<const h4*>(gp + 2 * kH);
     // next step's gates into the other tile, then refill that ring slot
     stage_gates((j + 1) % kGruPf, (step + 1) & 1);
-#if WK_GRU_ABL != 2
     load_gates((j + 1) % kGruPf, step + 1 + kGruPf);
-#endif
     int bq = u0 >> 2;
     asm volatile("" : "+v"(bq));   // re-read per step, not hoisted into 16 VGPRs
     const f32x4 b_r = gbias[0][bq], b_z = gbias[1][bq], bi_c = gbias[2][bq], bh_c = gbias[3][bq];
@@ -1158,15 +961,9 @@ __global__ __launch_bounds__(kGru16Threads, 4) void ctc_gru16_kernel(const __hal
     for (int i = 0; i < 4; ++i) {
       float hn = 0.0f;
       if (live) {
-#if WK_GRU_ABL == 1   // timing ablation: no transcendentals (wrong results)
-        const float r = 0.5f * ((float)gr[i] + ar[i] + b_r[i]);
-        const float z = 0.5f * ((float)gz[i] + az[i] + b_z[i]);
-        const float c = 0.25f * ((float)gc[i] + bi_c[i] + r * (an[i] + bh_c[i]));
-#else
         const float r = sigm((float)gr[i] + ar[i] + b_r[i]);
         const float z = sigm((float)gz[i] + az[i] + b_z[i]);
         const float c = tanh_fast((float)gc[i] + bi_c[i] + r * (an[i] + bh_c[i]));
-#endif
         hn = __builtin_fmaf(z, h[i] - c, c);   // (1 - z) c + z h
       }
       h[i] = hn;
@@ -1230,30 +1027,7 @@ constexpr int kGxHP = kH + 16;
 constexpr int kGxWaves = 8, kGxThreads = 64 * kGxWaves;
 typedef _Float16 h8x __attribute__((ext_vector_type(8)));
 constexpr float kNegLog2e = -1.4426950408889634f, kTwoLog2e = 2.8853900817779268f;
-
-#ifndef WK_GRU_VPM0
-#define WK_GRU_VPM0 2   // VALU per MFMA beside tile 1's h-part
-#endif
-#ifndef WK_GRU_LDSABL
-#define WK_GRU_LDSABL 0   // diagnostic: LDS access sites replaced by register values (bitmask; wrong results)
-#endif
-#ifndef WK_GRU_FLAGS
-#define WK_GRU_FLAGS 0   // experiment: per-wave step counters instead of the step barrier (see the kernel)
-#endif
-#ifndef WK_GRU_PRIO
-#define WK_GRU_PRIO 0   // experiment: issue priority 1 for the younger wave of each SIMD (waves 4-7)
-#endif
-#ifdef WK_GRU_STAMPS   // diagnostic build only (tools/debug/gru_stamps.py; needs -DWK_STAMPS): cycle sums per phase
-__device__ unsigned long long g_gru_stamps[2][kGxWaves][16];
-#define GRU_HIT(k)                                  \
-  do {                                              \
-    __builtin_amdgcn_sched_barrier(0);              \
-    _st.hit(k);                                     \
-    __builtin_amdgcn_sched_barrier(0);              \
-  } while (0)
-#else
-#define GRU_HIT(k) do {} while (0)
-#endif
+constexpr int kVpm0 = 2;   // VALU per MFMA beside tile 1's h-part (1 and 3 measured equal, 4: -2 %)
 
 // One element of the GRU cell on pre-scaled pre-activations (see above):
 // ar = -log2e (r pre-activation), az likewise, gn = 2 log2e (W_in x + b_in),
@@ -1279,15 +1053,11 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
   constexpr int XCH = kGxRows * DIN / 8;       // 16-byte chunks per x tile
   constexpr int XPT = (XCH + kGxThreads - 1) / kGxThreads;   // per thread
   // VALU per MFMA beside the x-part: the rest of the ~2 x 54 gate instructions
-  constexpr int VPM1 = (108 - 12 * WK_GRU_VPM0 + 6 * KX - 1) / (6 * KX) > 0 ? (108 - 12 * WK_GRU_VPM0 + 6 * KX - 1) / (6 * KX) : 1;
+  constexpr int VPM1 = (108 - 12 * kVpm0 + 6 * KX - 1) / (6 * KX) > 0 ? (108 - 12 * kVpm0 + 6 * KX - 1) / (6 * KX) : 1;
   __shared__ __attribute__((aligned(16))) _Float16 h16[2][kGxRows * kGxHP];
   __shared__ __attribute__((aligned(16))) _Float16 xt[2][kGxRows * XP];
   __shared__ __attribute__((aligned(16))) h8x wl[KXL > 0 ? 3 * kGxWaves * KXL * 64 : 1];
   __shared__ f32x4 gbias[4][kH / 4];
-  // WK_GRU_FLAGS: per-wave step counters replace the step barrier (flags[w] =
-  // steps wave w has finished, its state slice and x-tile writes complete);
-  // flags[8] is the abort word of the bounded spins
-  __shared__ __attribute__((aligned(16))) unsigned gflags[12];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int dir = blockIdx.y;
@@ -1321,7 +1091,6 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
     }
   }
   for (int i = tid; i < kGxRows * kGxHP; i += kGxThreads) h16[0][i] = (_Float16)0.0f;
-  if (tid < 12) gflags[tid] = 0u;
   if (tid < kH) {   // scaled biases: -log2e (b_ir + b_hr), -log2e (b_iz + b_hz), 2 log2e b_in, 2 log2e b_hn
     const float* bi = bih + dir * 3 * kH;
     const float* bh = bhh + dir * 3 * kH;
@@ -1350,7 +1119,7 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
 #pragma unroll
     for (int c = 0; c < XPT; ++c) {
       const int ch = tid + c * kGxThreads;
-      if (!(WK_GRU_LDSABL & 1)) *reinterpret_cast<uint4*>(&xt[buf][(ch / (DIN / 8)) * XP + (ch % (DIN / 8)) * 8]) = xv[slot][c];
+      *reinterpret_cast<uint4*>(&xt[buf][(ch / (DIN / 8)) * XP + (ch % (DIN / 8)) * 8]) = xv[slot][c];
     }
   };
   __syncthreads();   // gbias
@@ -1374,7 +1143,7 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
         an = xn[s < KXR ? s : 0];
       } else {
         const int sl = s - KXR;
-        if (WK_GRU_LDSABL & 32) { ar = xr[0]; az = xz[0]; an = xn[0]; } else {
+        {
         ar = wl[((0 * kGxWaves + wave) * (KXL > 0 ? KXL : 1) + sl) * 64 + lane];
         az = wl[((1 * kGxWaves + wave) * (KXL > 0 ? KXL : 1) + sl) * 64 + lane];
         an = wl[((2 * kGxWaves + wave) * (KXL > 0 ? KXL : 1) + sl) * 64 + lane];
@@ -1382,7 +1151,7 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const h8x xb = (WK_GRU_LDSABL & 2) ? xr[s % KXR] : *reinterpret_cast<const h8x*>(&xt[buf][(16 * q + n) * XP + 32 * s + 8 * lg]);
+        const h8x xb = *reinterpret_cast<const h8x*>(&xt[buf][(16 * q + n) * XP + 32 * s + 8 * lg]);
         g[q][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ar, xb, g[q][0], 0, 0, 0);
         g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, xb, g[q][1], 0, 0, 0);
         g[q][2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(an, xb, g[q][2], 0, 0, 0);
@@ -1399,7 +1168,7 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
   auto store_y = [&](int buf, int step_done, bool any) {   // the state after step step_done
     const int t = dir == 0 ? step_done : T - 1 - step_done;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(out + ((int64_t)t * B + b0) * (2 * kH), any ? (uint32_t)nrow * (2 * kH * 2) : 0u);
-    const uint4 v = (WK_GRU_LDSABL & 16) ? xv[0][0] : *reinterpret_cast<const uint4*>(&h16[buf][yn * kGxHP + 8 * yc]);
+    const uint4 v = *reinterpret_cast<const uint4*>(&h16[buf][yn * kGxHP + 8 * yc]);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), rs, yoff, 0, 0);
   };
   // prologue: x_0 and x_1 staged, x_2 / x_3 in the ring, gx of step 0
@@ -1415,72 +1184,7 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
   __syncthreads();   // x_0's tile is rewritten (with x_2) during step 0
   float h[2][4] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
   int cur = 0;
-#if WK_GRU_PRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
-#ifdef WK_GRU_STAMPS
-  wk::WkStamps _st;
-  _st.init();
-#endif
-#if WK_GRU_FLAGS
-  // wait until waves base .. base + 3 have finished `v` steps (bounded: on a
-  // timeout the abort word is set, every later wait returns at once and the
-  // results are wrong, but the grid drains)
-  auto wait4 = [&](int base, unsigned v) {
-    auto ld = [&](int i) { return __hip_atomic_load(&gflags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    for (unsigned it = 0;; ++it) {
-      if (min(min(ld(base), ld(base + 1)), min(ld(base + 2), ld(base + 3))) >= v) break;
-      if ((it & 15) == 15 && (it > (1u << 22) || ld(8))) {
-        __hip_atomic_store(&gflags[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    asm volatile("" ::: "memory");
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  };
-#endif
   auto step_body = [&](int step, f32x4 (&g)[2][3], f32x4 (&gn)[2][3], int slot) {
-#if WK_GRU_FLAGS
-    // slices 0-1 of the h-part (units 0-63) need only waves 0-3's state;
-    // the older waves start them while the younger finish the previous step
-    wait4(0, (unsigned)step);
-    f32x4 anh[2] = {b_hn, b_hn};
-    {
-      h8x hv0[2][2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) hv0[q][s] = *reinterpret_cast<const h8x*>(h16[cur] + (16 * q + n) * kGxHP + 8 * lg + 32 * s);
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          g[q][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[s], hv0[q][s], g[q][0], 0, 0, 0);
-          g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wz[s], hv0[q][s], g[q][1], 0, 0, 0);
-          anh[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wn[s], hv0[q][s], anh[q], 0, 0, 0);
-        }
-    }
-    wait4(4, (unsigned)step);
-    stage_x(slot, step & 1);
-    store_y(cur, step - 1, step > 0);
-    load_x(slot, step + 2 + kXPf);
-    h8x hv[2][2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) hv[q][s] = *reinterpret_cast<const h8x*>(h16[cur] + (16 * q + n) * kGxHP + 8 * lg + 32 * (s + 2));
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        g[q][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[s + 2], hv[q][s], g[q][0], 0, 0, 0);
-        g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wz[s + 2], hv[q][s], g[q][1], 0, 0, 0);
-        anh[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wn[s + 2], hv[q][s], anh[q], 0, 0, 0);
-      }
-#else
     // memory work of the step (independent of the MFMAs): x rows of step + 2
     // into the tile the previous step's x-part read, the previous step's
     // outputs (none at step 0), the ring slot refilled
@@ -1492,9 +1196,8 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
     for (int q = 0; q < 2; ++q) {
       const _Float16* hb = h16[cur] + (16 * q + n) * kGxHP + 8 * lg;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) hv[q][s] = (WK_GRU_LDSABL & 4) ? __builtin_bit_cast(h8x, xv[0][0]) : *reinterpret_cast<const h8x*>(hb + 32 * s);
+      for (int s = 0; s < 4; ++s) hv[q][s] = *reinterpret_cast<const h8x*>(hb + 32 * s);
     }
-    GRU_HIT(0);
     __builtin_amdgcn_sched_barrier(0);
     // h-part of this step onto the x-part (n's h-part apart, b_hn as its initial accumulator)
     f32x4 anh[2] = {b_hn, b_hn};
@@ -1506,7 +1209,6 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
         g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wz[s], hv[q][s], g[q][1], 0, 0, 0);
         anh[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wn[s], hv[q][s], anh[q], 0, 0, 0);
       }
-#endif
     // gate math of both tiles (tile 0 beside tile 1's h-part, tile 1 beside
     // the x-part of the next step; the last step's x-part reads a stale tile
     // and is discarded)
@@ -1520,12 +1222,12 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
         o[q][i] = (_Float16)hn;
       }
     xpart((step + 1) & 1, gn);
-    constexpr int kHp = WK_GRU_FLAGS ? 6 : 12;           // h-part MFMAs per tile in this region
+    constexpr int kHp = 12;           // h-part MFMAs per tile in this region
     __builtin_amdgcn_sched_group_barrier(0x008, kHp, 0);  // tile 0's h-part
 #pragma unroll
     for (int i = 0; i < kHp; ++i) {                       // tile 1's h-part || tile 0's gates
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, WK_GRU_VPM0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, kVpm0, 0);
     }
 #pragma unroll
     for (int i = 0; i < 6 * KX; ++i) {                    // x-part || tile 1's gates
@@ -1533,42 +1235,18 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
       __builtin_amdgcn_sched_group_barrier(0x002, VPM1, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    GRU_HIT(1);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-#if WK_GRU_HSINGLE   // (A/B) two single 8-byte writes (the compiler pairs them into ds_write2st64_b64)
-      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-      typedef volatile __attribute__((address_space(3))) u32x2 vlu2;
-      if (!(WK_GRU_LDSABL & 8)) *(vlu2*)&h16[cur ^ 1][(16 * q + n) * kGxHP + u0] = __builtin_bit_cast(u32x2, o[q]);
-#else
-      if (!(WK_GRU_LDSABL & 8)) *reinterpret_cast<uint2*>(&h16[cur ^ 1][(16 * q + n) * kGxHP + u0]) = __builtin_bit_cast(uint2, o[q]);
-#endif
+      *reinterpret_cast<uint2*>(&h16[cur ^ 1][(16 * q + n) * kGxHP + u0]) = __builtin_bit_cast(uint2, o[q]);
     }
     cur ^= 1;
-    GRU_HIT(2);
-#if WK_GRU_FLAGS
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's state slice, x-tile and output-copy LDS ops done
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (lane == 0) __hip_atomic_store(&gflags[wave], (unsigned)step + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#else
     __syncthreads();
-#endif
-    GRU_HIT(3);
   };
   for (int step = 0; step < T; step += 2) {
     step_body(step, ga, gb, 0);
     if (step + 1 < T) step_body(step + 1, gb, ga, 1);
   }
-#if WK_GRU_FLAGS
-  wait4(0, (unsigned)T);   // every wave's last state slice is in the image
-  wait4(4, (unsigned)T);
-#endif
   store_y(cur, T - 1, true);   // the last step's outputs
-#ifdef WK_GRU_STAMPS
-  if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0)
-    for (int k = 0; k < 16; ++k) atomicAdd(&g_gru_stamps[DIN == 128 ? 0 : 1][wave][k], _st.st[k]);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1769,40 +1447,11 @@ __global__ __launch_bounds__(256) void ctc_greedy_kernel(const int* __restrict__
 // order), so tokens do not depend on log-probs being requested.
 // ---------------------------------------------------------------------------
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-#ifndef WK_OUT_RF
-#define WK_OUT_RF 3      // 16-row MFMA tiles per wave (argmax-only kernel; the logits-storing one keeps 2: no spills)
-#endif
-#ifndef WK_OUT_WAVES
-#define WK_OUT_WAVES 8
-#endif
-#ifndef WK_OUT_SKEW
-#define WK_OUT_SKEW 1
-#endif
-#ifndef WK_OUT_DMA
-#define WK_OUT_DMA 1
-#endif
-#ifndef WK_OUT_PRIO
-#define WK_OUT_PRIO 0
-#endif
-#ifndef WK_OUT_BPIPE
-#define WK_OUT_BPIPE 0
-#endif
-#ifndef WK_OUT_EARLYDMA
-#define WK_OUT_EARLYDMA 0
-#endif
-// RING4: four W buffers, the leading waves' LDS-DMA two tiles ahead and one
-// barrier per two tiles (the barrier and its refill were ~10 % of a tile)
-#ifndef WK_OUT_RING4
-#define WK_OUT_RING4 0
-#endif
-static_assert(!WK_OUT_RING4 || (WK_OUT_DMA && !WK_OUT_EARLYDMA), "RING4 is a form of the LDS-DMA path");
-constexpr int kOutNB = WK_OUT_RING4 ? 4 : 2, kOutAhead = WK_OUT_RING4 ? 2 : 1;
-#ifndef WK_OUT_BN
-#define WK_OUT_BN 64     // W tile columns (64; 32 and 128 measured)
-#endif
-constexpr int kOutK = 2 * kH, kOutBN = WK_OUT_BN, kOutCF = kOutBN / 16, kOutPitch = kOutK, kOutRF = WK_OUT_RF,
-              kOutWaves = WK_OUT_WAVES;
-static_assert(kOutBN == 64 || ((kOutBN == 32 || kOutBN == 128) && !WK_OUT_EARLYDMA), "W tile width");
+// Double-buffered W tiles of 64 columns, 3 row tiles per wave, 8 waves (a
+// four-buffer ring with the LDS-DMA two tiles ahead, 32- and 128-column tiles,
+// 12 waves were measured slower: DESIGN 5.3).
+constexpr int kOutNB = 2, kOutAhead = 1;
+constexpr int kOutK = 2 * kH, kOutBN = 64, kOutCF = kOutBN / 16, kOutPitch = kOutK, kOutRF = 3, kOutWaves = 8;
 // W tile rows are 512 B with their 16-byte chunks XOR-swizzled by the row's
 // low 4 bits (chunk c of row n at c ^ (n & 15)): a ds_read_b128 B fragment
 // (row 16 cf + li, chunk 4 st + lg) then hits 16 distinct 4-bank windows in
@@ -1812,22 +1461,8 @@ __device__ __forceinline__ int out_chunk(int n, int c) { return c ^ (n & 15); }
 // (RF = 3, 48 rows per wave: each B fragment read from LDS feeds 3 MFMAs -- the
 // LDS bytes per MFMA were the limit at RF = 2; 246 VGPRs, still 2 waves per
 // SIMD: +3 % utterances/s.)
-constexpr int kOutPre = kOutBN * (kOutK / 8) / (64 * kOutWaves);
 constexpr int out_rf(bool logits) { return logits ? 2 : kOutRF; }
 constexpr int out_rows(bool logits) { return 16 * out_rf(logits) * kOutWaves; }
-static_assert(WK_OUT_DMA || kOutPre * 64 * kOutWaves == kOutBN * (kOutK / 8), "W tile chunks divide over the threads");
-
-#ifdef WK_OUT_STAMPS   // diagnostic build only (tools/debug/out_stamps.py; needs -DWK_STAMPS): cycle sums per phase
-__device__ unsigned long long g_out_stamps[kOutWaves][16];
-#define OUT_HIT(k)                                  \
-  do {                                              \
-    __builtin_amdgcn_sched_barrier(0);              \
-    _st.hit(k);                                     \
-    __builtin_amdgcn_sched_barrier(0);              \
-  } while (0)
-#else
-#define OUT_HIT(k) do {} while (0)
-#endif
 // KEYED (V <= 4096, so 4 NT <= 256): the running maximum carries its column
 // in the value's low 8 mantissa bits, so the epilogue is two VALU per value
 // and one v_max3_f32 per two values instead of compare + two selects per
@@ -1839,9 +1474,6 @@ __device__ unsigned long long g_out_stamps[kOutWaves][16];
 // A tagged value moves by < 2^-15 of itself: the first maximum is exact except
 // between logits that agree to within that (fp16 operands already put ~1e-3 of
 // noise on every logit); the tokens stay a function of the row alone.
-#ifndef WK_OUT_KEYED
-#define WK_OUT_KEYED 1
-#endif
 // m = max(m, k0, k1) on the tagged values (fmaxf would first canonicalise
 // each of them: they come from integer ops).  The tags are applied in C++, so
 // the compiler still places the wait states for reading MFMA results.
@@ -1893,7 +1525,6 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   const __amdgpu_buffer_rsrc_t wrs = make_rsrc(w, (uint32_t)V * kOutK * 2);
   const __amdgpu_buffer_rsrc_t brs = make_rsrc(bias, (uint32_t)V * 4);
   float pb = 0.0f;
-#if WK_OUT_DMA
   // W tile nt -> bt[nt & 1] by LDS-DMA (buffer_load ... lds), issued by waves
   // 0-3 after their MFMA phase: instruction i of wave w fills 1 KB = rows
   // 2 (8 w + i) and +1; lane L writes position L & 31 of its row, so it loads
@@ -1922,64 +1553,16 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #pragma unroll
     for (int i = 0; i < kDmaPer; ++i) dma_piece(nt, i);
   };
-#if WK_OUT_EARLYDMA
-  // (EARLYDMA) every wave issues 4 of the tile's 32 LDS-DMA pieces right after
-  // the barrier that freed the target buffer, a whole tile ahead of its use
-  constexpr int kDmaPerAll = kOutBN * kOutK * 2 / 1024 / kOutWaves;
-  int dma_off_all[kDmaPerAll];
-#pragma unroll
-  for (int i = 0; i < kDmaPerAll; ++i) {
-    const int q = wvu * kDmaPerAll + i, rr = 2 * q + (lane >> 5), c = (lane & 31) ^ (rr & 15);
-    dma_off_all[i] = rr * (kOutK * 2) + 16 * c;
-  }
-  auto dma_all = [&](int nt) {
-#pragma unroll
-    for (int i = 0; i < kDmaPerAll; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs,
-                                               (__attribute__((address_space(3))) void*)&bt[nt & 1][(wvu * kDmaPerAll + i) * 512],
-                                               16, dma_off_all[i], nt * (kOutBN * kOutK * 2), 0, 0);
-  };
-#endif
   auto fetch = [&](int nt) {   // the tile's bias (W comes by dma_w)
     if (wave0) pb = buf_load(brs, 4 * (nt * kOutBN + tid), 0);
   };
   auto stash = [&](int buf) {
     if (wave0 && tid < kOutBN) bsh[buf][tid] = f32x4{pb, pb, pb, pb};
   };
-#else
-  uint4 pre[kOutPre];
-  auto fetch = [&](int nt) {
-#pragma unroll
-    for (int i = 0; i < kOutPre; ++i) {
-      const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
-      pre[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             wrs, (nt * kOutBN + rr) * (kOutK * 2) + 16 * ch, 0, 0));
-    }
-    if (wave0) pb = buf_load(brs, 4 * (nt * kOutBN + tid), 0);
-  };
-  auto stash = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < kOutPre; ++i) {
-      const int u = tid + kOutWaves * 64 * i, rr = u >> 5, ch = u & 31;
-      *reinterpret_cast<uint4*>(&bt[buf][rr * kOutPitch + 8 * out_chunk(rr, ch)]) = pre[i];
-    }
-    if (wave0 && tid < kOutBN) bsh[buf][tid] = f32x4{pb, pb, pb, pb};
-  };
-#endif
   fetch(0);
   stash(0);
-#if WK_OUT_EARLYDMA
-  dma_all(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#elif WK_OUT_DMA
   dma_w(0);
-  for (int t = 1; t < kOutAhead && t < NT; ++t) {
-    fetch(t);
-    stash(t);
-    dma_w(t);
-  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
   __syncthreads();
   float mx[kOutRF][4];
   int ix[kOutRF][4];
@@ -1989,42 +1572,25 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
     for (int i = 0; i < 4; ++i) { mx[rf][i] = -INFINITY; ix[rf][i] = 0; }
-  // Skew (WK_OUT_SKEW): the second half of the waves (4-7, each the partner of
+  // Skew: the second half of the waves (4-7, each the partner of
   // a first-half wave on the same SIMD) runs one tile behind in its epilogue:
   // per tile it finishes tile nt - 1's argmax first, then issues tile nt's
   // MFMAs, while the first half issues tile nt's MFMAs and then its epilogue.
   // The barrier keeps all waves on one tile; the skew puts one wave's epilogue
   // VALU beside its partner's MFMAs instead of both SIMD waves alternating
   // all-MFMA and all-VALU phases in step.
-  // lagging: waves 4-7 (with 8 waves, one of the two waves of each SIMD; with
-  // 12, one of three)
-  const bool lag = WK_OUT_SKEW && ((__builtin_amdgcn_readfirstlane(wv) >> 2) & 1);
+  // lagging: waves 4-7, one of the two waves of each SIMD
+  const bool lag = (__builtin_amdgcn_readfirstlane(wv) >> 2) & 1;
   // The bias is the MFMAs' initial C operand (one ds_read_b128 of the
   // replicated bias per column tile), so the epilogue is compare + select.
   f32x4 acc[kOutRF][kOutCF];
   // (FULL: every column of the tile is < V -- all tiles but a ragged last
   // one -- so the per-lane bound check and its exec-mask blocks go)
-#ifndef WK_OUT_DMA_SPREAD
-#define WK_OUT_DMA_SPREAD 0   // (measured -2 to -4 %, not kept) the leading waves' LDS-DMA pieces issued between the epilogue's column blocks
-#endif
-  auto epilogue_t = [&](int tile, auto full, int dma_tile) __attribute__((always_inline)) {
+  auto epilogue_t = [&](int tile, auto full) __attribute__((always_inline)) {
     // column v = 64 tile + 16 cf + li, rows row0 + 16 rf + 4 lg + i
 #pragma unroll
     for (int cf = 0; cf < kOutCF; ++cf) {
-#if WK_OUT_DMA
-      if (dma_tile >= 0) {
-#pragma unroll
-        for (int i = cf * kDmaPer / kOutCF; i < (cf + 1) * kDmaPer / kOutCF; ++i) dma_piece(dma_tile, i);
-      }
-#endif
       const int v = tile * kOutBN + 16 * cf + li;
-#ifdef WK_OUT_ABL_EPI   // timing ablation only (wrong tokens): one max per column block instead of the argmax epilogue
-      if (true) {   // (the empty asm keeps every accumulator, hence every MFMA, alive at no cost)
-#pragma unroll
-        for (int rf = 0; rf < kOutRF; ++rf) asm volatile("" ::"v"(acc[rf][cf]));
-        continue;
-      }
-#endif
       if (KEYED) {
         const unsigned tag = 255u - (unsigned)(kOutCF * tile + cf);
         if (LOGITS) {
@@ -2064,121 +1630,20 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
       }
     }
   };
-  auto epilogue = [&](int tile, int dma_tile = -1) __attribute__((always_inline)) {
-    if ((tile + 1) * kOutBN <= V) epilogue_t(tile, std::true_type{}, dma_tile);
-    else epilogue_t(tile, std::false_type{}, dma_tile);
+  auto epilogue = [&](int tile) __attribute__((always_inline)) {
+    if ((tile + 1) * kOutBN <= V) epilogue_t(tile, std::true_type{});
+    else epilogue_t(tile, std::false_type{});
   };
-#if WK_OUT_PRIO
-  if (lag) __builtin_amdgcn_s_setprio(1);
-#endif
-#ifdef WK_OUT_STAMPS
-  wk::WkStamps _st;
-  _st.init();
-#endif
-#if WK_OUT_EARLYDMA
-  // B fragments and the bias C operands by inline-asm ds_read_b128 (the
-  // compiler would make any LDS read it sees wait for the LDS-DMA in flight):
-  // row 16 cf + li, chunk (4 st + lg) ^ li = 4 st ^ (lg ^ li), so with the
-  // buffer 512-byte aligned the lane's address for step st is P ^ 64 st, and
-  // the column tiles cf are immediate offsets of 16 rows (8 KB).
-  const unsigned lds_bt = (unsigned)(uintptr_t)(__attribute__((address_space(3))) _Float16*)&bt[0][0];
-  const unsigned lds_bs = (unsigned)(uintptr_t)(__attribute__((address_space(3))) f32x4*)&bsh[0][0];
-  const unsigned P0 = lds_bt + li * (kOutPitch * 2) + 16 * (lg ^ li);
-  for (int nt = 0; nt < NT; ++nt) {
-    if (nt + 1 < NT) {
-      fetch(nt + 1);
-      dma_all(nt + 1);
-    }
-    if (lag && nt > 0) epilogue(nt - 1);
-    OUT_HIT(0);
-    const unsigned pnt = P0 + (nt & 1) * (kOutBN * kOutPitch * 2), bnt = lds_bs + (nt & 1) * (kOutBN * 16) + 16 * li;
-    // step 0's fragments and the bias, waited for; then each step issues the
-    // next step's four reads before its own 12 MFMAs and waits after them
-    h8 bfc[4], bfn[4];
-    f32x4 c[4];
-    asm volatile(
-        "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:8192\n\t"
-        "ds_read_b128 %2, %8 offset:16384\n\tds_read_b128 %3, %8 offset:24576\n\t"
-        "ds_read_b128 %4, %9\n\tds_read_b128 %5, %9 offset:256\n\t"
-        "ds_read_b128 %6, %9 offset:512\n\tds_read_b128 %7, %9 offset:768\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(bfc[0]), "=&v"(bfc[1]), "=&v"(bfc[2]), "=&v"(bfc[3]), "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3])
-        : "v"(pnt), "v"(bnt)
-        : "memory");
-#pragma unroll
-    for (int st = 0; st < 8; ++st) {
-      if (st + 1 < 8) {
-        const unsigned ad = pnt ^ (64u * (st + 1));
-        asm volatile(
-            "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:8192\n\t"
-            "ds_read_b128 %2, %4 offset:16384\n\tds_read_b128 %3, %4 offset:24576"
-            : "=&v"(bfn[0]), "=&v"(bfn[1]), "=&v"(bfn[2]), "=&v"(bfn[3])
-            : "v"(ad)
-            : "memory");
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (st == 0) {
-#pragma unroll
-        for (int cf = 0; cf < 4; ++cf)
-#pragma unroll
-          for (int rf = 0; rf < kOutRF; ++rf)
-            acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][0], bfc[cf], c[cf], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int rf = 0; rf < kOutRF; ++rf)
-#pragma unroll
-          for (int cf = 0; cf < 4; ++cf)
-            acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bfc[cf], acc[rf][cf], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (st + 1 < 8) {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bfn[0]), "+v"(bfn[1]), "+v"(bfn[2]), "+v"(bfn[3])::"memory");
-#pragma unroll
-        for (int cf = 0; cf < 4; ++cf) bfc[cf] = bfn[cf];
-      }
-    }
-    OUT_HIT(1);
-    if (!lag && nt + 1 < NT) stash((nt + 1) & 1);
-    OUT_HIT(2);
-    if (!lag) epilogue(nt);
-    OUT_HIT(3);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this tile's LDS-DMA (issued at its start) done
-    OUT_HIT(4);
-    __syncthreads();
-    OUT_HIT(5);
-  }
-#else
   for (int nt = 0; nt < NT; ++nt) {
     if (nt + kOutAhead < NT) fetch(nt + kOutAhead);
     const _Float16* b = bt[nt & (kOutNB - 1)];
     if (lag && nt > 0) epilogue(nt - 1);
-    OUT_HIT(0);
-#if WK_OUT_BPIPE
-    // B fragments one k-step ahead: step st + 1's four reads are issued
-    // before step st's MFMAs (the compiler otherwise slots them among the last
-    // MFMAs of the step, ~1-4 MFMAs before their use)
-    h8 bfp[2][kOutCF];
-#pragma unroll
-    for (int cf = 0; cf < kOutCF; ++cf)
-      bfp[0][cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, lg));
-#endif
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
-#if WK_OUT_BPIPE
-      if (st + 1 < 8) {
-#pragma unroll
-        for (int cf = 0; cf < kOutCF; ++cf)
-          bfp[(st + 1) & 1][cf] =
-              *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, 4 * (st + 1) + lg));
-      }
-      __builtin_amdgcn_sched_barrier(0);   // the next step's reads stay ahead of this step's MFMAs
-      const h8* bf = bfp[st & 1];
-#else
       h8 bf[kOutCF];
 #pragma unroll
       for (int cf = 0; cf < kOutCF; ++cf)
         bf[cf] = *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, 4 * st + lg));
-#endif
       if (st == 0) {
 #pragma unroll
         for (int cf = 0; cf < kOutCF; ++cf) {
@@ -2194,40 +1659,15 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
           for (int cf = 0; cf < kOutCF; ++cf)
             acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf[cf], acc[rf][cf], 0, 0, 0);
       }
-#if WK_OUT_BPIPE
-      __builtin_amdgcn_sched_barrier(0);
-#endif
     }
-    OUT_HIT(1);
-#if WK_OUT_DMA
     if (!lag && nt + kOutAhead < NT) {   // after this wave's last LDS read of the period
       stash((nt + kOutAhead) & (kOutNB - 1));
-      if (!WK_OUT_DMA_SPREAD) dma_w(nt + kOutAhead);
+      dma_w(nt + kOutAhead);
     }
-#endif
-    OUT_HIT(2);
-    if (!lag) epilogue(nt, WK_OUT_DMA && WK_OUT_DMA_SPREAD && nt + 1 < NT && wvu < kDmaWaves ? nt + 1 : -1);
-    OUT_HIT(3);
-    // (RING4) tile nt + 2 is DMA'd into the buffer tile nt - 2 used: every wave
-    // left that tile behind a barrier (after nt - 1 for even nt, after nt - 2
-    // for odd), and the barrier after each odd tile publishes the tiles the
-    // two periods before it issued
-    if (!WK_OUT_RING4 || (nt & 1)) {
-#if WK_OUT_DMA
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // LDS-DMA done (the barrier's own wait omits it)
-#else
-      if (nt + 1 < NT) stash((nt + 1) & 1);
-#endif
-      OUT_HIT(4);
-      __syncthreads();
-    }
-    OUT_HIT(5);
+    if (!lag) epilogue(nt);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // LDS-DMA done (the barrier's own wait omits it)
+    __syncthreads();
   }
-#endif
-#ifdef WK_OUT_STAMPS
-  if (lane == 0 && blockIdx.x == 0 && !LOGITS)
-    for (int k = 0; k < 16; ++k) atomicAdd(&g_out_stamps[wv][k], _st.st[k]);
-#endif
   if (lag && NT > 0) epilogue(NT - 1);
   // first maximum across the 16 column lanes of each row
 #pragma unroll
@@ -2371,9 +1811,6 @@ struct wk_ctc {
   __half* out_w16;
   float* fft_win;       // [400] periodic Hann
   float* fft_tw;        // [20 k1][20 n2] W400^(n2 k1), complex
-  int *fb_start, *fb_len, *fb_off;
-  float* fb_w;
-  int n_fbw;            // CSR weight count (<= kFbMaxW)
   float* melw;          // ctc_logmel_fft2_kernel: per-lane padded mel weights x 1/4, [64][kMelW1] then [64][kMelW2]
   int* melws;           // their window start bins, [64] then [64]
   // workspaces (grown on demand)
@@ -2459,8 +1896,8 @@ void free_all(wk_ctc* c) {
   void* ts[] = {c->tr_feats, c->tr_part, c->tr_zs};
   for (void* q : ts) (void)hipFree(q);
   void* ps[] = {c->enc_w, c->enc_b, c->ln_g, c->ln_b, c->wih[0], c->wih[1], c->bih[0], c->bih[1], c->bhh[0],
-                c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->zero_b, c->fb_w, c->wih16[0], c->wih16[1],
-                c->out_w16, c->fft_win, c->fft_tw, c->fb_start, c->fb_len, c->fb_off, c->whh16_pk[0], c->whh16_pk[1],
+                c->bhh[1], c->whh_pk[0], c->whh_pk[1], c->out_w, c->out_b, c->zero_b, c->wih16[0], c->wih16[1],
+                c->out_w16, c->fft_win, c->fft_tw, c->whh16_pk[0], c->whh16_pk[1],
                 c->wih16x_pk[0], c->wih16x_pk[1], c->whh16x_pk[0], c->whh16x_pk[1], c->melw, c->melws};
   for (void* q : ps) (void)hipFree(q);
   if (c->blas) rocblas_destroy_handle(c->blas);
@@ -2621,12 +2058,6 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
       off[m] = (int)wv.size();
       for (int k = a0; k <= z; ++k) wv.push_back(fb[(size_t)k * kMels + m]);
     }
-    if (e == hipSuccess) e = upload(&c->fb_start, st.data(), kMels);
-    if (e == hipSuccess) e = upload(&c->fb_len, ln.data(), kMels);
-    if (e == hipSuccess) e = upload(&c->fb_off, off.data(), kMels);
-    if (e == hipSuccess) e = upload(&c->fb_w, wv.data(), wv.size());
-    c->n_fbw = (int)wv.size();
-    if (e == hipSuccess && c->n_fbw > kFbMaxW) e = hipErrorInvalidValue;   // LDS copy in ctc_logmel_fft_kernel
     {   // straight-line windows of ctc_logmel_fft2_kernel (see there)
       std::vector<float> mw((size_t)64 * (kMelW1 + kMelW2), 0.0f);
       std::vector<int> ws(128, 0);
@@ -2708,13 +2139,6 @@ wk_status ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n
     // read a device table instead of a possibly empty audio buffer
     const float* au = nv > 0 ? d_audio : c->fft_win;
     wk_status s = timed(c, WK_CTC_STAGE_LOGMEL, st, [&]() -> wk_status {
-#ifdef WK_LOGMEL_V1
-      const int64_t passes = (rows + kFftFrames - 1) / kFftFrames;
-      const int64_t blocks = (passes + kFftWaves - 1) / kFftWaves;
-      hipLaunchKernelGGL(ctc_logmel_fft_kernel, dim3((unsigned)(blocks < 8 * c->n_cu ? blocks : 8 * c->n_cu)), dim3(256),
-                         0, st, au, nv > 0 ? stride : (int64_t)0, nv, n_samples, T, rows, c->fft_win, c->fft_tw,
-                         c->fb_start, c->fb_len, c->fb_off, c->fb_w, c->n_fbw, d_feats);
-#else
       const int64_t passes2 = (rows + 2 * kF2Pairs - 1) / (2 * kF2Pairs);
       const int64_t blocks2 = (passes2 + kF2Waves - 1) / kF2Waves;
       const dim3 lg2((unsigned)(blocks2 < c->n_cu ? blocks2 : c->n_cu));
@@ -2724,7 +2148,6 @@ wk_status ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n
       else
         hipLaunchKernelGGL(ctc_logmel_fft2_kernel<false>, lg2, dim3(kF2Waves * 64), 0, st, au, nv > 0 ? stride : (int64_t)0,
                            nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->melw, c->melws, d_feats, (float4*)nullptr);
-#endif
       return WK_OK;
     });
     if (s == WK_OK)
@@ -2779,10 +2202,7 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
     if (rocblas_set_stream(c->blas, st) != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_set_stream");
     c->last_batch = batch;
     c->last_T = T;
-#ifndef WK_ENC_GRID
-#define WK_ENC_GRID 2   // encoder workgroups per CU (persistent; 2: 0.241 -> 0.21 ms against 8, 16 slower)
-#endif
-    const int enc_grid = (int)((rows + 63) / 64 < WK_ENC_GRID * c->n_cu ? (rows + 63) / 64 : WK_ENC_GRID * c->n_cu);
+    const int enc_grid = (int)((rows + 63) / 64 < 2 * c->n_cu ? (rows + 63) / 64 : 2 * c->n_cu);
     wk_status s = timed(c, WK_CTC_STAGE_ENCODER, st, [&]() -> wk_status {
       if (f16 && zs)
         hipLaunchKernelGGL(ctc_encoder16_kernel<true>, dim3(enc_grid), dim3(256), 0, st, d_feats, rows, c->enc_w,
@@ -2841,7 +2261,7 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
       // fused output layer + argmax; fp16 logits are written only for log_softmax
       const dim3 og((unsigned)((rows + out_rows(d_log_probs != nullptr) - 1) / out_rows(d_log_probs != nullptr)));
       s = timed(c, WK_CTC_STAGE_OUTPUT, st, [&]() -> wk_status {
-        const bool keyed = WK_OUT_KEYED && V <= 16 * 256;   // the tag holds kOutCF tile + cf in 8 bits
+        const bool keyed = 1 && V <= 16 * 256;   // the tag holds kOutCF tile + cf in 8 bits
         if (d_log_probs) {
           hipLaunchKernelGGL((keyed ? ctc_out_argmax16_kernel<true, true> : ctc_out_argmax16_kernel<true, false>), og,
                              dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, c->logits16, c->best);
@@ -2977,24 +2397,4 @@ wk_status wk_ctc_frame_argmax(wk_ctc* c, int64_t batch, int32_t T, int32_t* d_pr
 
 }  // extern "C"
 
-#ifdef WK_GRU_STAMPS
-extern "C" int wk_debug_gru_stamps(unsigned long long* host_out, int reset) {
-  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_gru_stamps), sizeof(g_gru_stamps)) != hipSuccess) return 1;
-  if (reset) {
-    static unsigned long long zero[2][kGxWaves][16];
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_gru_stamps), zero, sizeof(zero)) != hipSuccess) return 1;
-  }
-  return 0;
-}
-#endif
 
-#ifdef WK_OUT_STAMPS
-extern "C" int wk_debug_out_stamps(unsigned long long* host_out, int reset) {
-  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_out_stamps), sizeof(g_out_stamps)) != hipSuccess) return 1;
-  if (reset) {
-    static unsigned long long zero[kOutWaves][16];
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_out_stamps), zero, sizeof(zero)) != hipSuccess) return 1;
-  }
-  return 0;
-}
-#endif

@@ -26,18 +26,13 @@ using namespace wk;
 
 namespace {
 
-#ifdef WK_STAMPS
-// Diagnostic build only (tools/debug): per-wave cycle sums per phase.
+#ifdef WK_DIAG
+// Diagnostic builds only (-DWK_DIAG, tools/debug): per-wave cycle sums per phase.
 __device__ unsigned long long g_wk_stamps[16][16];
 #define WK_STAMP_INIT WkStamps _stamps; _stamps.init();
 #define WK_STAMP(k) _stamps.hit(k)
 #define WK_STAMP_FLUSH(w) do { if (lane == 0) for (int _k = 0; _k < 16; ++_k) atomicAdd(&g_wk_stamps[w][_k], _stamps.st[_k]); } while (0)
 #define WK_SP_ARG , &_stamps
-#elif defined(WK_ASM_MARKS)
-#define WK_STAMP_INIT
-#define WK_STAMP(k) asm volatile(";WKMARK st" #k)
-#define WK_STAMP_FLUSH(w) do {} while (0)
-#define WK_SP_ARG
 #else
 #define WK_STAMP_INIT
 #define WK_STAMP(k) do {} while (0)
@@ -45,21 +40,8 @@ __device__ unsigned long long g_wk_stamps[16][16];
 #define WK_SP_ARG
 #endif
 
-#ifdef WK_DEBUG_LOGMEL
-// Diagnostic build only: the log-mel image of every clip as the front-end
-// left it and as the DCT read it, [clip][40][64] each.
-__device__ float* g_dbg_fe;
-__device__ float* g_dbg_cnn;
-__device__ __forceinline__ void dbg_copy_logmel(float* dst, const float* lbuf, int64_t clip, int lane) {
-  if (!dst) return;
-  for (int m = 0; m < 40; ++m) dst[(clip * 40 + m) * 64 + lane] = lbuf[m * WK_LSTRIDE + lane];
-}
-#endif
 
 constexpr int NBF = 4;               // clips per CNN batch
-#ifndef WK_DCT_EAGER
-#define WK_DCT_EAGER 1               // MFMA DCT of the next batch's clips between this batch's conv phases
-#endif
 constexpr int kFusedBlock = 1024;    // 8 front-end + 8 CNN waves
 // LDS carve after the front-end's (wk_fe_dev.h): fixed tail, then the CNN
 // images [clip][t][ci] -- fp32, or bf16 for bf16 convolutions -- overlaying
@@ -108,6 +90,12 @@ enum { kConvF32 = 0, kConvBf16 = 1, kConvBf16x3 = 2 };
 constexpr int kDummyRowOff = (kImgEnd + 1) & ~1;          // even: its scratch is row + (63 & 1)
 constexpr int kFusedLds = kDummyRowOff + kPRow + 1;
 static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
+// The CNN role writes only inside [kGOff, kImgEnd) (pooled features,
+// classifier partials, the second log-mel buffer it reads, control words,
+// conv images); the front-end writes its power rows, the first log-mel
+// buffer and (frame 63) the dummy row: the two write sets are disjoint.
+static_assert(kPOff + kPSize <= kGOff && kLOff + kLSize <= kPOff && kImgEnd <= kDummyRowOff,
+              "CNN carve disjoint from the front-end's power rows, log-mel buffer and dummy row");
 
 // kCtrlLFree + w (w = CNN wave 0..7): clips whose log-mel buffer CNN wave w
 // has finished reading.  Per wave, not one shared count: the CNN waves are not
@@ -127,12 +115,8 @@ __device__ __forceinline__ unsigned lds_load(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-#ifndef WK_PRIO_FE
-#define WK_PRIO_FE 3      // issue priority of the front-end waves (the critical path; see the kernel)
-#endif
-#ifndef WK_SPIN_SLEEP
-#define WK_SPIN_SLEEP 2   // s_sleep argument (x64 cycles) between polls (2 measured >= 1)
-#endif
+constexpr int kPrioFe = 3;     // issue priority of the front-end waves (the critical path; see the kernel)
+constexpr int kSpinSleep = 2;  // s_sleep argument (x 64 cycles) between polls (2 measured >= 1; 4, 8 equal)
 
 // Spin until ctrl[idx] >= v.  On a timeout the workgroup's abort word is set
 // and every later spin returns at once.  Every poll is issue time taken from
@@ -145,7 +129,7 @@ __device__ __forceinline__ void spin_until(unsigned* ctrl, int idx, unsigned v) 
   if (lds_load(ctrl + idx) < v) {
     if (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     for (unsigned n = 0;; ++n) {
-      __builtin_amdgcn_s_sleep(WK_SPIN_SLEEP);
+      __builtin_amdgcn_s_sleep(kSpinSleep);
       if (lds_load(ctrl + idx) >= v) break;
       if ((n & 31) == 31 && (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort))) {
         __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -185,7 +169,7 @@ __device__ __forceinline__ void spin_until_all8(unsigned* ctrl, int idx, unsigne
   if (min8(ctrl, idx) < v) {
     if (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     for (unsigned n = 0;; ++n) {
-      __builtin_amdgcn_s_sleep(WK_SPIN_SLEEP);
+      __builtin_amdgcn_s_sleep(kSpinSleep);
       if (min8(ctrl, idx) >= v) break;
       if ((n & 31) == 31 && (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort))) {
         __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -219,7 +203,7 @@ __device__ __forceinline__ void signal_add(unsigned* ctrl, int idx, int lane) {
 template <typename T>
 __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio, int64_t n_mine,
                                         int64_t clip_stride, float* __restrict__ feats_out, int wave, int lane,
-                                        int exp_flags) {
+                                        int diag) {
   float* P = smem + kPOff;
   float* L = smem + kLOff;
   float* L1 = smem + kL1Off;
@@ -230,11 +214,6 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   const f2 w0 = fe_split_tw(j, 0);
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);
   const int fw = wave;   // frame slot of this wave (moving the edge frames to other waves measured neutral)
-#ifdef WK_ABL_NOEDGE
-  constexpr bool kEdge = false;   // timing ablation (tools/debug): edge frames take the plain path (wrong results)
-#else
-  constexpr bool kEdge = true;
-#endif
   const int64_t G = gridDim.x;
   unsigned gen = 0, p_wait = 0;
 
@@ -262,7 +241,7 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   };
   auto pf_ctx = [&](const T* p, bool ok, int r) -> PfCtx {
     const int fl = fw + 8 * r + slot_base;
-    return {make_rsrc(p, ok ? kClipBytes : 0u), 256 * fl - 160, kEdge && ((r == 0 && fw == 0) || (r == 1 && fw == 6))};
+    return {make_rsrc(p, ok ? kClipBytes : 0u), 256 * fl - 160, (r == 0 && fw == 0) || (r == 1 && fw == 6)};
   };
 
   Raw<T> pf;
@@ -275,14 +254,9 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
 #pragma unroll 1
     for (int r = 0; r < 2; ++r) {
       const int fl = fw + 8 * r + slot_base;   // == frame index t (one chunk per clip)
-      const bool general = kEdge && ((r == 0 && fw == 0) || (r == 1 && fw == 6));
-      if (exp_flags & 4) {   // alternate issue priority between the two front-end waves of a SIMD
-        if ((wave >= 4) == (r == 1)) __builtin_amdgcn_s_setprio(2); else __builtin_amdgcn_s_setprio(1);
-      } else if (exp_flags & 8) {
-        if ((wave >= 4) == (r == 1)) __builtin_amdgcn_s_setprio(1); else __builtin_amdgcn_s_setprio(0);
-      }
+      const bool general = (r == 0 && fw == 0) || (r == 1 && fw == 6);
       f2 a[16];
-#ifdef WK_STAMPS
+#ifdef WK_DIAG
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: time the wait for the prefetched audio apart
       WK_STAMP(11);
 #endif
@@ -300,29 +274,19 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
         if (k >= 0) {
           load_raw_part<true>(nx.rs, nx.base, j, kWinSamples, true, nx.general, pf, k);
         } else if (r == 0) {
-#ifndef WK_ABL_NOFEBAR   // timing ablation (tools/debug): no front-end barriers (wrong results)
-          spin_until<WK_PRIO_FE>(ctrl, kCtrlFeBar, p_wait);
-#endif
+          spin_until<kPrioFe>(ctrl, kCtrlFeBar, p_wait);
           WK_STAMP(9);
-#ifdef WK_DEBUG_LOGMEL
-          if (wave == 0 && i >= 1) dbg_copy_logmel(g_dbg_fe, (i - 1) & 1 ? L1 : L, (int64_t)blockIdx.x + G * (i - 1), lane);
-#endif
         }
       };
       WK_STAMP(1);
       float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
       fe_rest<true>(a, j, row, row + (fl & 1), tb, w0, tws, 0, pf_part WK_SP_ARG);
     }
-    if (exp_flags & 4) __builtin_amdgcn_s_setprio(1); else if (exp_flags & 8) __builtin_amdgcn_s_setprio(0);
-#ifndef WK_ABL_NOFEBAR
-    role_sync<WK_PRIO_FE>(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
-#endif
+    role_sync<kPrioFe>(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
     WK_STAMP(7);
-    if (i >= 2 && !(exp_flags & 1)) spin_until_all8<WK_PRIO_FE>(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
+    if (i >= 2 && !(diag & 1)) spin_until_all8<kPrioFe>(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
     WK_STAMP(10);
-#ifndef WK_ABL_NOMEL
     mel_dispatch<true>(wave, P + min(lane, kNFramesB - 1) * kPRow, (i & 1 ? L1 : L) + lane);
-#endif
     WK_STAMP(8);
     signal_add(ctrl, kCtrlLReady, lane);
     // Split barrier: arrive now, wait before this wave next writes a power
@@ -476,13 +440,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
 #pragma unroll
     for (int s = 0; s < 6; ++s) w3b[s] = frag_bf(kPbW3 + (cw * 6 + s) * kBfFrag);
   }
-#ifndef WK_W3_RESIDENT
-#define WK_W3_RESIDENT 1   // fp32 conv3 taps: in VGPRs across batches (1), re-read from L2 per pass (0), or loaded
-                           // once per batch as conv2 ends (2: no DCT-time spills, but 5 % slower than 1 with its
-                           // 18 spilled VGPRs, which are reloaded from L1 at the sync points)
-#endif
-  constexpr bool kW3Batch = CM == kConvF32 && WK_W3_RESIDENT == 2;
-  if constexpr (CM == kConvF32 && WK_W3_RESIDENT == 1) {
+  if constexpr (CM == kConvF32) {
 #pragma unroll
     for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
   }
@@ -494,7 +452,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
   // now (fused: its buffer goes back to the front-end a whole batch earlier;
   // the double buffer otherwise stalled the front-end ~13 % of the time in fp32).
   auto try_eager = [&](int64_t b) {
-    if (!WK_DCT_EAGER || cw >= NBF || eager_done) return;
+    if (!1 || cw >= NBF || eager_done) return;
     const int64_t i = (b + 1) * NBF + cw;
     if (i >= n_mine) return;
     if (src.ready(i)) {
@@ -505,11 +463,8 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
   // ReLU -> classifier.2 (64 -> 1) of batch bb from the classifier.0 partials:
   // lane = (o group q = lane>>2, clip = lane&3).  Run by one wave, deferred to
   // just after the next batch's first barrier (one barrier per batch fewer).
-#ifndef WK_FC2_WAVE
-#define WK_FC2_WAVE 0
-#endif
   auto fc2 = [&](int64_t bb) {
-    if (cw != WK_FC2_WAVE) return;
+    if (cw != 0) return;
     int ln = lane;
     asm volatile("" : "+v"(ln));
     const int cl = ln & (NBF - 1), q = ln >> 2;
@@ -629,19 +584,13 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
         f32x4 m[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-#ifndef WK_ABL_NOCONV2
         conv_wino_v<2, F1_CIP, 1>(F1, w2, (cl * I1_TP + 2 * li) * F1_CIP + 4 * lk, m);
-#endif
         epi_wino_pool<F2_CIP, I2_TP, 15>(m, F2, co0, cl, 0, lane);
       }
     }
-    if constexpr (kW3Batch) {
-#pragma unroll
-      for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
-    }
     WK_STAMP(3);
     role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);
-    if (!kW3Batch) try_eager(b);   // (w3 is live from here to the end of conv3)
+    try_eager(b);
     WK_STAMP(4);
 
     // conv3: co tile cw, the 4 clips; GAP -> G[128][4].
@@ -664,14 +613,8 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
                                           acc_a, acc_b);
         } else {
           // Winograd: one tile of 16 pair columns = 8 pairs of clip ca, 8 of clip cb
-          if (!WK_W3_RESIDENT) {
-#pragma unroll
-            for (int s = 0; s < 48; ++s) w3[s] = buf_load(rs, lv, 4 * (kPkW3 + (cw * 48 + s) * 64));
-          }
           f32x4 m[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-#ifndef WK_ABL_NOCONV3   // timing ablations (tools/debug): conv MFMAs skipped (wrong results)
           conv_wino_v<4, F2_CIP, 1>(F2, w3, ((ca + (li >> 3)) * I2_TP + 2 * (li & 7)) * F2_CIP + 4 * lk, m);
-#endif
           epi_wino_gap<NBF>(m, Gp, co0, ca, lane);
           continue;
         }
@@ -698,9 +641,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       const int kh = cw >> 2;
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-#ifndef WK_ABL_NOFC1
         acc = mfma4(wf1[s], Gp[(64 * kh + 4 * s + lk) * NBF + (li & (NBF - 1))], acc);
-#endif
       }
       if (li < NBF) {
 #pragma unroll
@@ -731,7 +672,7 @@ struct LogmelSrc {
   unsigned* ctrl;
   float* feats_out;
   int64_t clip_base, clip_step;
-  int cw, lane, exp_flags;
+  int cw, lane, diag;
   // Log-mel buffer release (kCtrlLFree + w): wave w < NBF reads only clips
   // w, w + NBF, w + 2 NBF, ...; its word holds the next clip it will read, so
   // every clip below it is released.  Waves >= NBF read none.
@@ -745,20 +686,17 @@ struct LogmelSrc {
   // ready-count read (LDS operations of a wave then complete in order).
   __device__ __forceinline__ bool ready(int64_t i) const {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const bool r = (exp_flags & 2) ||
+    const bool r = (diag & 2) ||
                    __builtin_amdgcn_readfirstlane(lds_load(ctrl + kCtrlLReady)) >= 8u * (unsigned)(i + 1);
     asm volatile("" ::: "memory");
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     return r;
   }
   __device__ __forceinline__ void wait(int64_t i) const {
-    if (!(exp_flags & 2)) spin_until<0>(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
+    if (!(diag & 2)) spin_until<0>(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
   }
   __device__ __forceinline__ void load(int64_t i, int slot) const {
     float* fo = FEATS ? feats_out + (clip_base + clip_step * i) * (13 * kNFramesB) : nullptr;
-#ifdef WK_DEBUG_LOGMEL
-    dbg_copy_logmel(g_dbg_cnn, smem + (i & 1 ? kL1Off : kLOff), clip_base + clip_step * i, lane);
-#endif
     dct_cmvn_clip<CM>(smem + (i & 1 ? kL1Off : kLOff), slot, smem + kF0Off,
                       reinterpret_cast<uint16_t*>(smem + kB0Off), reinterpret_cast<uint16_t*>(smem + kX0Off), fo,
                       lane);
@@ -784,10 +722,10 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
                                                                  const uint16_t* __restrict__ wbf,
                                                                  float* __restrict__ logits,
                                                                  float* __restrict__ feats_out, unsigned* err,
-                                                                 int exp_flags) {
+                                                                 int diag) {
   __shared__ __attribute__((aligned(16))) float smem[kFusedLds];
-#ifndef WK_DEBUG_EXPERIMENTS
-  exp_flags = 0;   // the product kernel folds every experiment branch away (~20 scalar instructions per round)
+#ifndef WK_DIAG
+  diag = 0;   // role isolation (1 = front-end role only, 2 = CNN role only) in -DWK_DIAG builds; folded away here
 #endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -799,19 +737,15 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
   // The front-end role is the critical path: static issue priority over the
   // CNN role measured +0.5-0.9 % (priority 1-3); the reverse (CNN over
   // front-end) measured -13 %.
-  if (WK_PRIO_FE > 0 && wave < 8) __builtin_amdgcn_s_setprio(WK_PRIO_FE);
+  if (wave < 8) __builtin_amdgcn_s_setprio(kPrioFe);
   if (wave < 8) {
-#ifndef WK_EXPERIMENT_NO_FE
-    if (!(exp_flags & 2)) fe_role<T>(smem, audio, n_mine, clip_stride, feats_out, wave, lane, exp_flags);
-#endif
+    if (!(diag & 2)) fe_role<T>(smem, audio, n_mine, clip_stride, feats_out, wave, lane, diag);
   } else {
-#ifndef WK_EXPERIMENT_NO_CNN
-    if (!(exp_flags & 1)) {
+    if (!(diag & 1)) {
       LogmelSrc<CM, FEATS> src = {smem, reinterpret_cast<unsigned*>(smem + kCtrlOff), feats_out, (int64_t)blockIdx.x,
-                                  (int64_t)gridDim.x, 0, 0, exp_flags};
+                                  (int64_t)gridDim.x, 0, 0, diag};
       cnn_role<CM>(smem, wts, wbf, n_mine, (int64_t)blockIdx.x, (int64_t)gridDim.x, logits, wave - 8, lane, src);
     }
-#endif
   }
   report_abort(reinterpret_cast<unsigned*>(smem + kCtrlOff), err, lane);
 }
@@ -891,26 +825,9 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_cnn_fused_kernel(const floa
 
 }  // namespace
 
-#ifdef WK_DEBUG_LOGMEL
-extern "C" int wk_debug_logmel_set(float* fe, float* cnn) {
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_fe), &fe, sizeof(fe)) != hipSuccess) return 1;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_cnn), &cnn, sizeof(cnn)) != hipSuccess) return 1;
-  return 0;
-}
-#endif
 
-#ifdef WK_EPI_CHECK
-extern "C" int wk_debug_epi_get(unsigned* out8, int reset) {
-  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_epi_bad), 8 * sizeof(unsigned)) != hipSuccess) return 1;
-  if (reset) {
-    static unsigned zero[8];
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_epi_bad), zero, sizeof(zero)) != hipSuccess) return 1;
-  }
-  return 0;
-}
-#endif
 
-#ifdef WK_STAMPS
+#ifdef WK_DIAG
 extern "C" int wk_debug_stamps(unsigned long long* host_out, int reset) {
   if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wk_stamps), sizeof(g_wk_stamps)) != hipSuccess) return 1;
   if (reset) {
@@ -925,7 +842,7 @@ namespace wk {
 
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
                         const uint16_t* wbf, int conv_mode, float* logits, float* feats_or_null, int grid_cap,
-                        hipStream_t stream, unsigned* err, int exp_flags) {
+                        hipStream_t stream, unsigned* err, int diag) {
   if (batch == 0) return hipSuccess;
   const int grid = (int)(batch < grid_cap ? batch : grid_cap);
   const dim3 g(grid), blk(kFusedBlock);
@@ -934,10 +851,10 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
   do {                                                                                                         \
     if (feats_or_null)                                                                                         \
       hipLaunchKernelGGL((wk_fused_kernel<T, CM, true>), g, blk, 0, stream, (const T*)audio, batch, clip_stride, \
-                         w, wbf, logits, feats_or_null, err, exp_flags);                                            \
+                         w, wbf, logits, feats_or_null, err, diag);                                               \
     else                                                                                                       \
       hipLaunchKernelGGL((wk_fused_kernel<T, CM, false>), g, blk, 0, stream, (const T*)audio, batch,            \
-                         clip_stride, w, wbf, logits, nullptr, err, exp_flags);                                     \
+                         clip_stride, w, wbf, logits, nullptr, err, diag);                                        \
   } while (0)
   if (i16) {
     if (conv_mode == kConvBf16) WK_FUSED_LAUNCH(int16_t, kConvBf16);

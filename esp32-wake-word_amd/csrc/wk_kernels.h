@@ -42,8 +42,8 @@ hipError_t launch_frontend(bool mode_b, bool i16, const void* audio, int64_t bat
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
                         const uint16_t* wbf, int conv_mode, float* logits, float* feats_or_null, int grid_cap, hipStream_t stream,
                         unsigned* err,        // host-visible protocol error word (see wk_fused_kernel), may be null
-                        int exp_flags = 0);   // timing experiments (-DWK_DEBUG_EXPERIMENTS builds only): 1 = FE role
-                                              // only, 2 = CNN role only; wrong logits
+                        int diag = 0);   // role isolation (-DWK_DIAG builds only): 1 = FE role only,
+                                         // 2 = CNN role only; wrong logits
 
 // CNN on caller features (wk_fused.hip, the fused kernel's CNN role fed from
 // HBM): feats [B][13][63] -> logits [B]; conv_mode as launch_fused.

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Ad-hoc rocprofv3 PMC passes (one counter group per run, no trace domains):
 #   bash tools/debug/pmc_groups.sh <outdir> <groups-file> [bench args...]
-# Environment (e.g. WAKEWORD_FUSED_EXP, honoured by -DWK_DEBUG_EXPERIMENTS builds only) passes through to bench.py.
+# Environment (e.g. WAKEWORD_FUSED_EXP, honoured by -DWK_DIAG builds only) passes through to bench.py.
 set -o pipefail
 R=$(cd "$(dirname "$0")/../.." && pwd)
 OUT=$(realpath -m "$1"); GF=$(realpath "$2"); shift 2

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Issue-level PMC (tools/debug/groups_issue.txt) of the fused kernel per role:
 # CONFIGS="prec:exp ..." (exp 0 = fused, 1 = front-end role alone, 2 = CNN role
-# alone; needs the -DWK_DEBUG_EXPERIMENTS variant build/var_exp).
+# alone; needs the -DWK_DIAG variant build/var_exp).
 export WAKEWORD_LIB=$PWD/esp32-wake-word_amd/build/var_exp/libwakeword.so
 for cfg in ${CONFIGS:-fp32:0 fp32:1 fp32:2 bf16:0}; do
   p=${cfg%%:*}; x=${cfg##*:}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Role isolation of the fused kernel (timing only; logits are wrong):
-# WAKEWORD_FUSED_EXP is honoured only by libraries built with -DWK_DEBUG_EXPERIMENTS
-# (bash tools/debug/build_variant.sh exp -DWK_DEBUG_EXPERIMENTS; WAKEWORD_LIB=...var_exp/libwakeword.so).
+# WAKEWORD_FUSED_EXP is honoured only by libraries built with -DWK_DIAG
+# (bash tools/debug/build_variant.sh exp -DWK_DIAG; WAKEWORD_LIB=...var_exp/libwakeword.so).
 # for each precision, FE role alone (exp 1), CNN role alone (exp 2), both (0).
 # PRECS / AUDIO select the precisions and the sample type (f32 / i16).
 R=$(cd "$(dirname "$0")/../.." && pwd)
