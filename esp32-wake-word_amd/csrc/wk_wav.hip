@@ -162,8 +162,9 @@ wk_status wk_augment(const float* in, int32_t n, float speed, float volume, floa
   if (!in || !out || n <= 0 || out_len <= 0 || !(speed > 0.0f) || !(volume > 0.0f) || noise_level < 0.0f)
     return invalid("wk_augment: bad arguments");
   // speed: F.interpolate(size=int(n * speed), mode='linear', align_corners=False), then pad/trim to out_len
-  const int32_t m = (int32_t)((double)n * (double)speed);
-  if (m <= 0) return invalid("wk_augment: speed too small");
+  const double md = (double)n * (double)speed;   // (range-checked before the cast: UBSan, tests/test_sanitizers.py)
+  if (!(md >= 1.0) || md > 2147483647.0) return invalid("wk_augment: speed out of range");
+  const int32_t m = (int32_t)md;
   const float scale = (float)n / (float)m;
   for (int32_t i = 0; i < out_len; ++i) {
     float v = noise_level > 0.0f ? noise_level * gauss(seed, 0u, (uint32_t)i) : 0.0f;   // pad_audio's noise pad

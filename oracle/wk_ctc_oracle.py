@@ -91,12 +91,15 @@ class GRUCTC(nn.Module):
         return torch.nn.functional.log_softmax(self.output_layer(y), dim=-1)
 
 
-def make_model(vocab: int, seed: int = 0, hidden: int = 128) -> GRUCTC:
+def make_model(vocab: int, seed: int = 0, hidden: int = 128, out_scale: float = 4.0) -> GRUCTC:
+    """Seeded GRU_CTC_Model (ctc.py:119-146 has no trained weights to load).
+    out_scale multiplies the output layer's default nn.Linear init: 4 gives
+    the greedy path margins (random init is near-uniform); 1 keeps the init."""
     torch.manual_seed(seed)
     m = GRUCTC(vocab, hidden)
-    # Scale the classifier up so the greedy path has margins (random init is near-uniform).
-    with torch.no_grad():
-        m.output_layer.weight.mul_(4.0)
+    if out_scale != 1.0:
+        with torch.no_grad():
+            m.output_layer.weight.mul_(out_scale)
     return m.eval()
 
 

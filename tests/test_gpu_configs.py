@@ -171,3 +171,61 @@ def test_config5_ctc_full_batch():
     agree = float((pred3.numpy() == p).mean())
     assert agree > 0.999, agree
     assert int(ln3.min()) >= 0 and int(ln3.max()) <= T
+
+
+def _edit_distance(a, b):
+    """Levenshtein distance between two token sequences."""
+    prev = list(range(len(b) + 1))
+    for i, x in enumerate(a, 1):
+        cur = [i] + [0] * len(b)
+        for j, y in enumerate(b, 1):
+            cur[j] = min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (x != y))
+        prev = cur
+    return prev[-1]
+
+
+# (out_scale, bounds): the oracle model's output layer at 4x its default init
+# (the margins the other config-5 tests rely on) and at the default nn.Linear
+# init (near-uniform logits over V = 4000: near-ties everywhere).  Bounds:
+# minimum exact-sequence match rate, maximum mean edit distance per utterance
+# (in tokens), minimum frame-argmax agreement.
+CTC_DECISION_BOUNDS = {4.0: (0.90, 0.25, 0.995), 1.0: (0.25, 6.0, 0.95)}
+
+
+@pytest.mark.parametrize("out_scale", [4.0, 1.0])
+def test_config5_decision_parity(out_scale):
+    """Config 5's product output is the token sequence (decode_predictions,
+    ctc.py:453-471).  For 64 utterances spread over the B = 4096 batch, the
+    one-call fp16 path bench_ctc.py times (wk_ctc_transcribe) against
+    greedy_decode of the torch-CPU oracle: the exact-sequence match rate, the
+    mean token edit distance per utterance and the frame-argmax agreement are
+    printed and held to CTC_DECISION_BOUNDS."""
+    import torch
+    import wakeword
+    from oracle import wk_ctc_oracle as CO
+    B, V, n = 4096, 4000, 48000
+    T = 1 + n // 160
+    m = CO.make_model(V, seed=0, out_scale=out_scale)
+    g = wakeword.CTCModel(m.state_dict(), V, precision="fp16")
+    audio = wakeword.synth_clips(1234, 0, B, n)
+    tok, ln = g.decode_audio(audio, n_samples=n)
+    pred = g.frame_argmax(B, T).cpu()
+    tok, ln = tok.cpu().numpy(), ln.cpu().numpy()
+    idx = torch.linspace(0, B - 1, 64).long()
+    x_s = torch.from_numpy(audio[idx.cuda()].cpu().numpy())
+    with torch.no_grad():
+        ref_lp = m(CO.features(x_s))
+    ref_seqs = CO.greedy_decode(ref_lp)
+    exact, dist, ntok = 0, 0, 0
+    for j, b in enumerate(idx.tolist()):
+        got = tok[b, :ln[b]].tolist()
+        exact += got == ref_seqs[j]
+        dist += _edit_distance(got, ref_seqs[j])
+        ntok += len(ref_seqs[j])
+    frame_agree = float((pred[idx] == ref_lp.argmax(-1)).float().mean())
+    match, mean_dist = exact / len(idx), dist / len(idx)
+    print(f"\nconfig5 decisions (out_scale {out_scale}): exact-sequence match {match:.4f} "
+          f"({exact}/{len(idx)}), mean edit distance {mean_dist:.3f} tokens per utterance "
+          f"(oracle mean length {ntok / len(idx):.1f}), frame-argmax agreement {frame_agree:.5f}")
+    lo_match, hi_dist, lo_frame = CTC_DECISION_BOUNDS[out_scale]
+    assert match >= lo_match and mean_dist <= hi_dist and frame_agree >= lo_frame, (match, mean_dist, frame_agree)
