@@ -129,12 +129,19 @@ def main():
     fused = f16 and cnt[STAGES.index("proj0")] == 0
     if fused:
         # projection fused into the recurrence: the layer reads its input rows
-        # instead of the gate inputs and does the projection's flops too
+        # instead of the gate inputs and does the projection's flops too.  Each
+        # direction's recurrence reads every input row once, at opposite ends
+        # of the sequence (step t forward, step T-1-t backward), so the
+        # compulsory reads are 2 x the input: the two reads of a row lie ~|2t-T|
+        # steps (4.2 MB of layer-1 input per step) apart, beyond L2 and, but for
+        # the middle rows, the Infinity Cache.  Reading the input once needs the
+        # unfused projection, whose [rows][768] gate tensor (3 x the input's
+        # bytes at layer 1, 6 x at layer 0) is written and read back.
         rows = B * T
         for l, din in ((0, H), (1, 2 * H)):
             by_g, fl_g = work[f"gru{l}"]
             by_p, fl_p = work[f"proj{l}"]
-            work[f"gru{l}"] = (rows * din * 2 + rows * 2 * H * 2 + 6 * H * din * 2, fl_g + fl_p)
+            work[f"gru{l}"] = (2 * rows * din * 2 + rows * 2 * H * 2 + 6 * H * din * 2, fl_g + fl_p)
     traffic, traffic_src = load_traffic(args.precision)
     kernels = {}
     for i, s in enumerate(STAGES):

@@ -38,7 +38,7 @@ __device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g,
     s += dpp<0x4E>(s);
     s += dpp<0x141>(s);
     s += dpp<0x140>(s);
-    if (tt == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s / 7.0f;
+    if (tt == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s * (1.0f / 7.0f);
   }
 }
 
@@ -246,7 +246,7 @@ __device__ __forceinline__ void epi_wino_gap(const f32x4 (&m)[4], float* __restr
     s += dpp<0xB1>(s);    // 8-lane sum: quad_perm xor 1, xor 2, row_half_mirror
     s += dpp<0x4E>(s);
     s += dpp<0x141>(s);
-    if (p == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s / 7.0f;
+    if (p == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s * (1.0f / 7.0f);
   }
 }
 

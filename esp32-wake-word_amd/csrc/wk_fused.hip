@@ -96,6 +96,15 @@ static_assert(kFusedLds * 4 <= 163840, "fused LDS budget");
 // buffer and (frame 63) the dummy row: the two write sets are disjoint.
 static_assert(kPOff + kPSize <= kGOff && kLOff + kLSize <= kPOff && kImgEnd <= kDummyRowOff,
               "CNN carve disjoint from the front-end's power rows, log-mel buffer and dummy row");
+// Inside the window, the front-end writes the second log-mel buffer and the
+// control words; the CNN role's writes (pooled features, classifier partials,
+// every precision's image set) sit in ranges that miss it.
+static_assert(kGOff + 128 * NBF <= kFcpOff && kFcpOff + 2 * 64 * NBF <= kL1Off && kL1Off + kLSize <= kCtrlOff &&
+                  kCtrlOff + 16 <= kImgOff,
+              "pooled features | partials | log-mel buffer 1 | control words, in that order, disjoint");
+static_assert(kF2End <= kImgEnd && kB2Off + NBF * I2_TP * I2_CIP / 2 <= kImgEnd &&
+                  kX2Off + NBF * I2_TP * X2_CIP / 2 <= kImgEnd,
+              "every precision's conv images end inside [kImgOff, kImgEnd)");
 
 // kCtrlLFree + w (w = CNN wave 0..7): clips whose log-mel buffer CNN wave w
 // has finished reading.  Per wave, not one shared count: the CNN waves are not
@@ -344,18 +353,21 @@ __device__ __forceinline__ void dct_cmvn_clip(const float* __restrict__ lbuf, in
   }
   const bool v3 = li != 15;   // tile 3 column 15 = frame 63 (padding)
   float mean[4], inv[4];
+  // Reciprocal constants, v_sqrt_f32 and v_rcp_f32 (each <= 1 ulp) instead of
+  // IEEE divisions and the libm square root: 12 divisions per clip had
+  // compiled to ~10-instruction div_scale/div_fmas/div_fixup sequences.
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float x3 = v3 ? d[3][r] : 0.0f;
-    mean[r] = row_sum16((d[0][r] + d[1][r]) + (d[2][r] + x3)) / (float)kNFramesB;
+    mean[r] = row_sum16((d[0][r] + d[1][r]) + (d[2][r] + x3)) * (1.0f / kNFramesB);
     float dv[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) dv[nt] = d[nt][r] - mean[r];
     dv[3] = v3 ? dv[3] : 0.0f;
     const float q = row_sum16((dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]));
-    float sd = sqrtf(q / (float)(kNFramesB - 1));
+    float sd = __builtin_amdgcn_sqrtf(q * (1.0f / (kNFramesB - 1)));
     sd = sd == 0.0f ? 1.0f : sd;   // rows 13-15 (all zero) land here and stay 0
-    inv[r] = 1.0f / (sd + 1e-8f);
+    inv[r] = __builtin_amdgcn_rcpf(sd + 1e-8f);
   }
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
