@@ -295,7 +295,15 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
     WK_STAMP(7);
     if (i >= 2 && !(diag & 1)) spin_until_all8<kPrioFe>(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
     WK_STAMP(10);
-    mel_dispatch<true>(wave, P + min(lane, kNFramesB - 1) * kPRow, (i & 1 ? L1 : L) + lane);
+    {
+      // The row base stays opaque (one VGPR with kPOff in it), so the mel's
+      // power reads take bin offsets as read2 immediates; folded into the
+      // immediates, kPOff pushed them past read2's 255-dword reach and every
+      // pair of reads cost a v_add_u32 for its address.
+      int prow = kPOff + min(lane, kNFramesB - 1) * kPRow;
+      asm volatile("" : "+v"(prow));
+      mel_dispatch<true>(wave, smem + prow, (i & 1 ? L1 : L) + lane);
+    }
     WK_STAMP(8);
     signal_add(ctrl, kCtrlLReady, lane);
     // Split barrier: arrive now, wait before this wave next writes a power
