@@ -294,34 +294,13 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
     sc = f2{e, e};
     sc0 = esp_pack ? (j == 0 ? f2{1.0f / 2048.0f, 0.0f} : sc) : sc;  // j==0, k2==0: bins 0 and 256
   }
-  // bin 128 (k2 = 8, column 0): X[128] = conj Z[128], so |U|^2 = 4 |Z[128]|^2.
-  float p128;
   {
+    // bin 128 (k2 = 8, column 0): X[128] = conj Z[128], so |U|^2 = 4 |Z[128]|^2.
     const f2 z = c[dft16_out(8)];
-    p128 = 4.0f * __builtin_fmaf(z.x, z.x, z.y * z.y);
+    float p128 = 4.0f * __builtin_fmaf(z.x, z.x, z.y * z.y);
     if constexpr (!MODE_B) p128 = __builtin_fmaf(p128, sc.x, 1e-12f);
+    if (j == 0) row[128] = p128;
   }
-#if WK_SPLIT_LDS
-  // Partner exchange through the frame's row (free once the transpose reads
-  // are issued): slot s = 8..15 of lane j at f2 index 16 (s - 8) + j, so the
-  // writes and the reads (lane-uniform offsets, lanes permuted within 128 B)
-  // are conflict-free.  Lane j != 0 reads slot 15 - k2 of lane 16 - j; lane 0
-  // reads its own slot 16 - k2 (k2 >= 1) and keeps c[0] for k2 = 0.
-  f2 zp[8];
-  {
-    f2* xe = reinterpret_cast<f2*>(xs);
-    wave_lds_sync();
-#pragma unroll
-    for (int s = 8; s < 16; ++s) xe[(s - 8) * 16 + j] = c[dft16_out(s)];
-    wave_lds_sync();
-    const int pb = j ? 16 - j : 16;
-#pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2) zp[k2] = xe[(7 - k2) * 16 + pb];
-    wave_lds_sync();   // every partner read is issued before the power writes reuse the row
-    if (j == 0) zp[0] = c[dft16_out(0)];
-  }
-#endif
-  if (j == 0) row[128] = p128;
   // The eight k2 chains are ~20 dependent packed ops each; run them G at a
   // time, stage by stage, so independent ops fill each other's latency
   // (left to itself the scheduler emitted them back to back, one chain at a
@@ -335,9 +314,6 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
       const int k2 = k0 + t;
       if (k2 > 7) continue;
       const f2 zk = c[dft16_out(k2)];
-#if WK_SPLIT_LDS
-      const f2 zq = zp[k2];
-#else
       const f2 sv = c[dft16_out(15 - k2)];
       const f2 own = c[dft16_out((16 - k2) & 15)];
       // row_mirror (lane j <- 15 - j), then row_shr:1 (lane j <- j - 1) with
@@ -348,7 +324,6 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
                                                         0x111, 0xF, 0xF, false));
       zq.y = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), __float_as_int(dpp<0x140>(sv.y)),
                                                         0x111, 0xF, 0xF, false));
-#endif
       S[t] = fma2(zq, f2{1.0f, -1.0f}, zk);
       D[t] = fma2(zq, f2{-1.0f, 1.0f}, zk);
     }

@@ -5,7 +5,7 @@
 # summarise with:  python tools/pmc_census.py <outdir>
 set -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
-OUT=${1:-$R/gpurun_out/census}; shift
+OUT=$(realpath -m "${1:-$R/gpurun_out/census}"); shift
 ARGS=${@:-"--steps 2 --warmup 1 --no-cpu-baseline"}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
