@@ -185,7 +185,7 @@ __device__ __forceinline__ void epi_pool_bf3(const f32x4& acc, uint16_t* __restr
 // front-end cycle).  The pair is also exactly maxpool(2)'s window, so the
 // epilogue pools in-lane.  MFMA columns = pairs; lane (n, q) reads rows
 // 2n..2n+3 at ci = 16 cb + 4 q + j (the ci-blocked K order of conv_pair_v, so
-// the same packed taps g0, g1, g2 serve; G1, G2 are formed per step).
+// the same packed taps g0, G1, g2 serve; G2 is formed per step).
 // boff = this lane's element of row 2n; image pitch CIP = 4 mod 8 keeps the
 // stride-2 row reads conflict-free.
 template <int CB, int CIP, int CHUNK = 0>
@@ -204,10 +204,12 @@ __device__ __forceinline__ void conv_wino_v(const float* __restrict__ img, const
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float g0 = w[4 * cb + j], g1 = w[4 * (CB + cb) + j], g2 = w[4 * (2 * CB + cb) + j];
+      // packed taps g0, G1 = (g0 + g1 + g2) / 2, g2 (pack_fragments); G2 =
+      // (g0 - g1 + g2) / 2 = (g0 + g2) - G1, two VALU per step
+      const float g0 = w[4 * cb + j], G1 = w[4 * (CB + cb) + j], g2 = w[4 * (2 * CB + cb) + j];
       float sg = g0 + g2;
-      asm volatile("" : "+v"(sg));   // keep G1, G2 per step: hoisted out of the caller's loops they cost 2 VGPRs each
-      const float G1 = 0.5f * (sg + g1), G2 = 0.5f * (sg - g1);
+      asm volatile("" : "+v"(sg));   // keep G2 per step: hoisted out of the caller's loops it costs a VGPR per step
+      const float G2 = sg - G1;
       m[0] = mfma4(g0, d[0][j] - d[2][j], m[0]);
       m[1] = mfma4(G1, d[1][j] + d[2][j], m[1]);
       m[2] = mfma4(G2, d[2][j] - d[1][j], m[2]);

@@ -229,7 +229,9 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   // Static frame assignment: wave w, round r, lane group g takes frame
   // w + 8r + 16(g&1) + 32(g>>1) (groups 0/1 16 frames apart: disjoint LDS
   // banks).  A dynamic hand-out through an LDS counter was measured slower:
-  // the atomic's return latency lands on the prefetch path.
+  // the atomic's return latency lands on the prefetch path.  Both edge
+  // frames in wave 0's round 0 (one reflected-index round per clip instead
+  // of two) measured -1 %: that wave then finishes last at the clip barrier.
   //
   // Prefetch context of a round, built once per round: the clip's buffer
   // resource and whether the round holds a reflected edge frame (frame 0 in

@@ -79,7 +79,8 @@ constexpr int kNumWeights = kOffF2 + 64;        // 40224
 // v_mfma_f32_16x16x4_f32 (row = l&15), so a wave loads one fragment with one
 // coalesced 256-byte load.
 //   conv ([clip][t][ci] images): step s = 4 (tap * CB + cb) + j, lane group
-//     q = l>>4 feeds ci = 16 cb + 4 q + j at that tap (Cin padded to 16).
+//     q = l>>4 feeds ci = 16 cb + 4 q + j at that tap (Cin padded to 16);
+//     taps 0 and 2 are g0, g2, tap 1 the Winograd tap G1 = (g0 + g1 + g2) / 2.
 //   classifier.0: k = 4s + q.
 constexpr int kPkW1 = 0;                        // [2 tiles][12 s][64]
 constexpr int kPkW2 = kPkW1 + 2 * 12 * 64;      // [4][24][64]
@@ -141,7 +142,14 @@ inline void pack_fragments(const float* w, float* pk) {
         for (int l = 0; l < 64; ++l) {
           const int g = s >> 2, j = s & 3, tap = g / cb_n, cb = g % cb_n;
           const int co = 16 * t + (l & 15), ci = 16 * cb + 4 * (l >> 4) + j;
-          pk[off + (t * nsteps + s) * 64 + l] = ci < cin ? w[wbase + (co * cin + ci) * 3 + tap] : 0.0f;
+          float v = 0.0f;
+          if (ci < cin) {
+            const float* g = w + wbase + (co * cin + ci) * 3;
+            // tap 1 holds the Winograd F(2,3) tap G1 = (g0 + g1 + g2) / 2; the
+            // kernel forms G2 = (g0 + g2) - G1 (conv_wino_v)
+            v = tap == 1 ? (float)(0.5 * ((double)g[0] + (double)g[1] + (double)g[2])) : g[tap];
+          }
+          pk[off + (t * nsteps + s) * 64 + l] = v;
         }
   };
   conv_blocked(kPkW1, 2, 13, 16, kOffW1);

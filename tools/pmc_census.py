@@ -34,10 +34,23 @@ def main():
         for c in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
             if c in m:
                 out["share_" + c] = m[c] / m["SQ_WAVE_CYCLES"]
+    # SIMD-time shares (counters summed over the chip): SQ_ACTIVE_INST_* and
+    # SQ_WAVE_CYCLES count quad-cycles per wave; SQ_VALU_MFMA_BUSY_CYCLES counts
+    # cycles; GRBM_GUI_ACTIVE / 8 XCDs = the kernel's cycles; 1,024 SIMDs.
+    if "GRBM_GUI_ACTIVE" in m:
+        kc = m["GRBM_GUI_ACTIVE"] / 8.0
+        simd_cycles = 1024 * kc
+        out["kernel_cycles"] = kc
+        if "SQ_ACTIVE_INST_VALU" in m:
+            out["simd_share_valu_active"] = 4 * m["SQ_ACTIVE_INST_VALU"] / simd_cycles
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+            out["simd_share_mfma_busy"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles
+        if "SQ_ACTIVE_INST_ANY" in m:
+            out["simd_share_any_active"] = 4 * m["SQ_ACTIVE_INST_ANY"] / simd_cycles
     for k in sorted(per):
         print(f"{k:28s} {per[k]:12.1f} per window")
     for k, v in out.items():
-        if k.startswith(("share_", "valu_plus", "fp32_vector")):
+        if k.startswith(("share_", "valu_plus", "fp32_vector", "simd_share", "kernel_cycles")):
             print(f"{k:28s} {v:12.4f}")
     if "--json" in sys.argv:
         json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
