@@ -230,11 +230,20 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     const int ta_cur = ta_next;   // frame index of this pass's first row in its utterance
     // stage 1: lane (g, n2 = q): DFT-20 over n1 of z[20 n1 + n2] = w (x_a + i x_b)
     f2 v[20];
+    {
+      // All twenty window reads first (one LDS wait), then the products; the
+      // memory clobber after them keeps the next pass's loads behind the
+      // products.  (A clobber per product had serialised the window reads:
+      // twenty LDS round trips per pass, each waited for.)
+      float wn[20];
 #pragma unroll
-    for (int n1 = 0; n1 < 20; ++n1) {
-      const float wn = L.win[20 * n1 + q];
-      v[n1] = f2{ra[n1], rb[n1]} * f2{wn, wn};
-      asm volatile("" ::"v"(v[n1].x), "v"(v[n1].y) : "memory");   // ahead of the next pass's loads
+      for (int n1 = 0; n1 < 20; ++n1) wn[n1] = L.win[20 * n1 + q];
+#pragma unroll
+      for (int n1 = 0; n1 < 20; ++n1) {
+        v[n1] = f2{ra[n1], rb[n1]} * f2{wn[n1], wn[n1]};
+        asm volatile("" ::"v"(v[n1].x), "v"(v[n1].y));
+      }
+      asm volatile("" ::: "memory");   // ahead of the next pass's loads
     }
     load_pair(ps + pstep, ra, rb);
     dft20(v);
@@ -247,9 +256,26 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
     wave_lds_sync();
     // stage 2: lane (g, k1 = q) gathers column k1: lane groups g start at
     // 40 g x 25 = 40 g mod 64 dwords, so half-waves touch disjoint banks
+    // (software-pipelined in chunks of four: the reads of chunk c + 1 issue
+    // before chunk c's twiddle products, so only the first chunk's reads are
+    // waited for in full)
     if (lact) {
+      constexpr int CK = 4;
+      f2 ab[2][CK], tb[2][CK];
+      auto ldc = [&](int c, int b) {
 #pragma unroll
-      for (int n2 = 0; n2 < 20; ++n2) v[n2] = cmul2(LM_R(A, (g * 20 + n2) * kA2Pitch + q), L.tw[q][n2]);
+        for (int k = 0; k < CK; ++k) {
+          ab[b][k] = LM_R(A, (g * 20 + CK * c + k) * kA2Pitch + q);
+          tb[b][k] = L.tw[q][CK * c + k];
+        }
+      };
+      ldc(0, 0);
+#pragma unroll
+      for (int c = 0; c < 20 / CK; ++c) {
+        if (c + 1 < 20 / CK) ldc(c + 1, (c + 1) & 1);
+#pragma unroll
+        for (int k = 0; k < CK; ++k) v[CK * c + k] = cmul2(ab[c & 1][k], tb[c & 1][k]);
+      }
     }
     dft20(v);   // Z[q + 20 k2] in v[k2]
     // exchange (the A reads of this wave are done: one wave's LDS ops complete in order)
@@ -301,17 +327,37 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
       f2 c0 = {0.0f, 0.0f}, c1 = {0.0f, 0.0f}, c2 = {0.0f, 0.0f};
       typedef const volatile __attribute__((address_space(3))) f2 vf2;
 #define LM_RD(p, i) (*(vf2*)((p) + (i)))
+      // Software-pipelined one tap ahead: the volatile reads issue in source
+      // order, so tap j + 1's six reads are written before tap j's FMAs (in two
+      // separate loops the second set's reads had been issued one at a time,
+      // each waited for: ~21 serial LDS round trips per pass).
+      f2 x1[2][3], x2[2][3];
+      auto ld = [&](int j, int b) {
+        if (j < kMelW1) {
+          x1[b][0] = LM_RD(p1, j);
+          x1[b][1] = LM_RD(p1, kP2Pitch + j);
+          x1[b][2] = LM_RD(p1, 2 * kP2Pitch + j);
+        }
+        if (j < kMelW2) {
+          x2[b][0] = LM_RD(p2, j);
+          x2[b][1] = LM_RD(p2, kP2Pitch + j);
+          x2[b][2] = LM_RD(p2, 2 * kP2Pitch + j);
+        }
+      };
+      static_assert(kMelW1 >= kMelW2, "the first window is the longer one");
+      ld(0, 0);
 #pragma unroll
       for (int j = 0; j < kMelW1; ++j) {
-        a0 = fma2(LM_RD(p1, j), f2{mw1[j], mw1[j]}, a0);
-        a1 = fma2(LM_RD(p1, kP2Pitch + j), f2{mw1[j], mw1[j]}, a1);
-        a2 = fma2(LM_RD(p1, 2 * kP2Pitch + j), f2{mw1[j], mw1[j]}, a2);
-      }
-#pragma unroll
-      for (int j = 0; j < kMelW2; ++j) {
-        c0 = fma2(LM_RD(p2, j), f2{mw2[j], mw2[j]}, c0);
-        c1 = fma2(LM_RD(p2, kP2Pitch + j), f2{mw2[j], mw2[j]}, c1);
-        c2 = fma2(LM_RD(p2, 2 * kP2Pitch + j), f2{mw2[j], mw2[j]}, c2);
+        if (j + 1 < kMelW1) ld(j + 1, (j + 1) & 1);
+        const int b = j & 1;
+        a0 = fma2(x1[b][0], f2{mw1[j], mw1[j]}, a0);
+        a1 = fma2(x1[b][1], f2{mw1[j], mw1[j]}, a1);
+        a2 = fma2(x1[b][2], f2{mw1[j], mw1[j]}, a2);
+        if (j < kMelW2) {
+          c0 = fma2(x2[b][0], f2{mw2[j], mw2[j]}, c0);
+          c1 = fma2(x2[b][1], f2{mw2[j], mw2[j]}, c1);
+          c2 = fma2(x2[b][2], f2{mw2[j], mw2[j]}, c2);
+        }
       }
 #undef LM_RD
       float cv[6] = {c0.x, c0.y, c1.x, c1.y, c2.x, c2.y};
@@ -1127,6 +1173,10 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
   asm volatile("" : "+v"(bq));
   const f32x4 b_r = gbias[0][bq], b_z = gbias[1][bq], b_n = gbias[2][bq], b_hn = gbias[3][bq];
   // x-part of one step from the x tile `buf` into g[tile][gate] (bias as the initial accumulator)
+  // The operands of k-step s + 1 (the two x-tile B fragments and, for layer
+  // 1's k >= 128, the three W_ih A fragments from LDS) are read before k-step
+  // s's MFMAs, so each step's reads have the previous step's MFMAs to land
+  // behind (read one at a time, each had been waited for in full).
   auto xpart = [&](int buf, f32x4 (&g)[2][3]) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -1134,27 +1184,29 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
       g[q][1] = b_z;
       g[q][2] = b_n;
     }
+    h8x xb[2][2], wa[2][3];
+    auto ldx = [&](int s, int st) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) xb[st][q] = *reinterpret_cast<const h8x*>(&xt[buf][(16 * q + n) * XP + 32 * s + 8 * lg]);
+      if (s >= KXR) {
+        const int sl = s - KXR;
+#pragma unroll
+        for (int gt = 0; gt < 3; ++gt) wa[st][gt] = wl[((gt * kGxWaves + wave) * (KXL > 0 ? KXL : 1) + sl) * 64 + lane];
+      }
+    };
+    ldx(0, 0);
 #pragma unroll
     for (int s = 0; s < KX; ++s) {
-      h8x ar, az, an;
-      if (s < KXR) {
-        ar = xr[s < KXR ? s : 0];
-        az = xz[s < KXR ? s : 0];
-        an = xn[s < KXR ? s : 0];
-      } else {
-        const int sl = s - KXR;
-        {
-        ar = wl[((0 * kGxWaves + wave) * (KXL > 0 ? KXL : 1) + sl) * 64 + lane];
-        az = wl[((1 * kGxWaves + wave) * (KXL > 0 ? KXL : 1) + sl) * 64 + lane];
-        an = wl[((2 * kGxWaves + wave) * (KXL > 0 ? KXL : 1) + sl) * 64 + lane];
-        }
-      }
+      if (s + 1 < KX) ldx(s + 1, (s + 1) & 1);
+      const int st = s & 1;
+      const h8x ar = s < KXR ? xr[s < KXR ? s : 0] : wa[st][0];
+      const h8x az = s < KXR ? xz[s < KXR ? s : 0] : wa[st][1];
+      const h8x an = s < KXR ? xn[s < KXR ? s : 0] : wa[st][2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const h8x xb = *reinterpret_cast<const h8x*>(&xt[buf][(16 * q + n) * XP + 32 * s + 8 * lg]);
-        g[q][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ar, xb, g[q][0], 0, 0, 0);
-        g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, xb, g[q][1], 0, 0, 0);
-        g[q][2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(an, xb, g[q][2], 0, 0, 0);
+        g[q][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ar, xb[st][q], g[q][0], 0, 0, 0);
+        g[q][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, xb[st][q], g[q][1], 0, 0, 0);
+        g[q][2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(an, xb[st][q], g[q][2], 0, 0, 0);
       }
     }
   };
@@ -1229,10 +1281,21 @@ __global__ __launch_bounds__(kGxThreads, 1) void ctc_gru16x_kernel(const __half*
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, kVpm0, 0);
     }
+    // x-part || tile 1's gates: the LDS operands of k-step s + 1 (0x100: DS
+    // reads) are placed ahead of k-step s's six MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // (KXR >= 1: k-step 0's A fragments are in VGPRs)
 #pragma unroll
-    for (int i = 0; i < 6 * KX; ++i) {                    // x-part || tile 1's gates
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, VPM1, 0);
+    for (int s = 0; s < KX; ++s) {
+      if (s + 1 < KXR) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      } else if (s + 1 < KX) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, VPM1, 0);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
