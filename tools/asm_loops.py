@@ -6,8 +6,34 @@ import re
 import sys
 from collections import Counter
 
-sys.path.insert(0, __import__("os").path.dirname(__file__))
-from asm_phases import cls  # noqa: E402  (instruction classes)
+
+
+def cls(op, line):
+    """Instruction class of one ISA line (op = its mnemonic)."""
+    if op.startswith("v_mfma"):
+        return "mfma"
+    if op.startswith("v_pk_"):
+        return "valu_pk"
+    if op.startswith("v_") and ("_dpp" in op or " row_" in line or "quad_perm" in line):
+        return "dpp"
+    if op.startswith(("v_log", "v_exp", "v_rcp", "v_sqrt", "v_rsq", "v_sin", "v_cos")):
+        return "trans"
+    if op.startswith("v_cndmask"):
+        return "cndmask"
+    if op.startswith("v_"):
+        return "valu"
+    if op.startswith("ds_"):
+        return "lds"
+    if op.startswith(("global_", "buffer_", "flat_", "scratch_")):
+        return "vmem"
+    if op.startswith("s_waitcnt"):
+        return "waitcnt"
+    if op.startswith("s_nop"):
+        return "nop"
+    if op.startswith("s_"):
+        return "salu"
+    return "other"
+
 
 path, key = sys.argv[1], sys.argv[2]
 mn = int(sys.argv[3]) if len(sys.argv) > 3 else 200
