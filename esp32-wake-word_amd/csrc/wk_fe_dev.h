@@ -337,14 +337,14 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
       pw[t] = fma2(uvx, uvx, uvy * uvy);
       if constexpr (!MODE_B) pw[t] = fma2(pw[t], k2 == 0 ? sc0 : sc, f2{1e-12f, 1e-12f});
     }
+    // the group's low bins first, then its high bins: same-base stores 16
+    // dwords apart, back to back, which the compiler pairs into ds_write2_b32
 #pragma unroll
-    for (int t = 0; t < G; ++t) {
-      const int k2 = k0 + t;
-      if (k2 > 7) continue;
-      const int kb = j + 16 * k2;
-      row[kb] = pw[t].x;
-      row[256 - kb] = pw[t].y;
-    }
+    for (int t = 0; t < G; ++t)
+      if (k0 + t <= 7) row[j + 16 * (k0 + t)] = pw[t].x;
+#pragma unroll
+    for (int t = 0; t < G; ++t)
+      if (k0 + t <= 7) row[256 - j - 16 * (k0 + t)] = pw[t].y;
   }
   WK_FE_HIT(6);
 }
