@@ -123,24 +123,39 @@ constexpr unsigned kSpinLimit = 1u << 22;
 __device__ __forceinline__ unsigned lds_load(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// The same word as a wave-uniform (SGPR) value: every lane reads the same
+// address, and a spin's exit tests on an SGPR compile to a scalar compare and
+// branch instead of the exec-mask bookkeeping of a divergent loop exit.
+__device__ __forceinline__ unsigned lds_load_u(const unsigned* p) {
+  return __builtin_amdgcn_readfirstlane(lds_load(p));
+}
 
 constexpr int kPrioFe = 3;     // issue priority of the front-end waves (the critical path; see the kernel)
 constexpr int kSpinSleep = 2;  // s_sleep argument (x 64 cycles) between polls (2 measured >= 1; 4, 8 equal)
 
-// Spin until ctrl[idx] >= v.  On a timeout the workgroup's abort word is set
-// and every later spin returns at once.  Every poll is issue time taken from
-// the other waves of the SIMD, so a waiting wave drops to issue priority 0
-// (PRIO = the role's priority, restored on exit) and polls the abort word only
-// every 32nd iteration.
-template <int PRIO>
-__device__ __forceinline__ void spin_until(unsigned* ctrl, int idx, unsigned v) {
+// Spin until ready() (a wave-uniform test of an LDS word).  On a timeout the
+// workgroup's abort word is set and every later spin returns at once.  Every
+// poll is issue time taken from the other waves of the SIMD, so a waiting wave
+// drops to issue priority 0 (PRIO = the role's priority, restored on exit),
+// polls four times per loop trip and checks the bound and the abort word only
+// every 32nd poll: per poll a sleep, the read, its wait, one readfirstlane, a
+// scalar compare and branch (the former one-poll loop with its two exits
+// compiled to ~19 instructions of exec-mask bookkeeping per poll).
+template <int PRIO, typename F>
+__device__ __forceinline__ void spin_on(unsigned* ctrl, const F& ready) {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  if (lds_load(ctrl + idx) < v) {
+  if (!ready()) {
     if (PRIO > 0) __builtin_amdgcn_s_setprio(0);
-    for (unsigned n = 0;; ++n) {
+    for (unsigned n = 4;; n += 4) {
       __builtin_amdgcn_s_sleep(kSpinSleep);
-      if (lds_load(ctrl + idx) >= v) break;
-      if ((n & 31) == 31 && (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort))) {
+      if (ready()) break;
+      __builtin_amdgcn_s_sleep(kSpinSleep);
+      if (ready()) break;
+      __builtin_amdgcn_s_sleep(kSpinSleep);
+      if (ready()) break;
+      __builtin_amdgcn_s_sleep(kSpinSleep);
+      if (ready()) break;
+      if ((n & 31) == 0 && (n >= kSpinLimit || lds_load_u(ctrl + kCtrlAbort))) {
         __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         break;
       }
@@ -149,6 +164,12 @@ __device__ __forceinline__ void spin_until(unsigned* ctrl, int idx, unsigned v) 
   }
   asm volatile("" ::: "memory");
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// Spin until ctrl[idx] >= v.
+template <int PRIO>
+__device__ __forceinline__ void spin_until(unsigned* ctrl, int idx, unsigned v) {
+  spin_on<PRIO>(ctrl, [=] { return lds_load_u(ctrl + idx) >= v; });
 }
 
 // Barrier among the 8 waves of one role (LDS counter; s_barrier would also
@@ -174,21 +195,7 @@ __device__ __forceinline__ unsigned min8(const unsigned* ctrl, int idx) {
 }
 template <int PRIO>
 __device__ __forceinline__ void spin_until_all8(unsigned* ctrl, int idx, unsigned v) {
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  if (min8(ctrl, idx) < v) {
-    if (PRIO > 0) __builtin_amdgcn_s_setprio(0);
-    for (unsigned n = 0;; ++n) {
-      __builtin_amdgcn_s_sleep(kSpinSleep);
-      if (min8(ctrl, idx) >= v) break;
-      if ((n & 31) == 31 && (n >= kSpinLimit || lds_load(ctrl + kCtrlAbort))) {
-        __hip_atomic_store(ctrl + kCtrlAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        break;
-      }
-    }
-    if (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
-  }
-  asm volatile("" ::: "memory");
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  spin_on<PRIO>(ctrl, [=] { return __builtin_amdgcn_readfirstlane(min8(ctrl, idx)) >= v; });
 }
 
 // Publish a per-wave progress value once this wave's LDS ops are complete.
