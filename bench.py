@@ -217,18 +217,21 @@ def load_traffic(precision="fp32"):
 def init_rank(args, env, torch, dist):
     """This rank's (world, rank, local device, shared) from torchrun's
     environment, with the process group formed: nccl (RCCL) with the rank's
-    own device as `device_id`, or gloo.  shared = more ranks than visible
-    GPUs (a gloo rehearsal of the N>1 path on one GPU): the line then carries
-    no throughput."""
+    own device as `device_id`, or gloo.  shared = more ranks on THIS node
+    (LOCAL_WORLD_SIZE, torchrun's per-node count; WORLD_SIZE when unset) than
+    visible GPUs (a gloo rehearsal of the N>1 path on one GPU): the line then
+    carries no throughput.  A multi-node job with one rank per GPU on every
+    node is not a rehearsal."""
     world = int(env.get("WORLD_SIZE", "1"))
     rank = int(env.get("RANK", "0"))
     local = int(env.get("LOCAL_RANK", "0"))
+    local_world = int(env.get("LOCAL_WORLD_SIZE", str(world)))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     ndev = torch.cuda.device_count()
     if args.dist_backend == "nccl" and local >= ndev:
         raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPU(s) visible")
-    shared = world > ndev
+    shared = local_world > ndev
     local = local % ndev   # (gloo rehearsal: ranks may share a GPU)
     torch.cuda.set_device(local)
     if world > 1:

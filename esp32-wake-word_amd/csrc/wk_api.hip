@@ -23,6 +23,8 @@ struct wk_handle {
   std::mutex ws_mu;
   hipEvent_t ws_free;
   bool ws_used;
+  bool ws_poisoned;      // the workspace's last use could neither be recorded nor drained: later
+                         // staged forwards refuse to run (WK_ERR_HIP) rather than race it
   float* d_weights;      // packed WK_NUM_WEIGHTS floats, or nullptr (front-end only handle)
   float* d_packed;       // fragment-major weights (wk::pack_fragments) for the fused kernel
   float* d_feats_ws;     // feature workspace for the unfused path
@@ -267,6 +269,8 @@ static wk_status forward_impl(wk_handle* h, const void* d_audio, int32_t dtype, 
     std::unique_lock<std::mutex> ws_lock(h->ws_mu, std::defer_lock);
     if (!d_feats_or_null && batch > 0) {
       ws_lock.lock();
+      if (h->ws_poisoned)
+        return wk::fail(WK_ERR_HIP, "wk_forward: the feature workspace's previous use could not be ordered or drained");
       hipError_t e = h->ws_used ? hipStreamWaitEvent((hipStream_t)stream, h->ws_free, 0) : hipSuccess;
       if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent(workspace)");
     }
@@ -289,7 +293,11 @@ static wk_status forward_impl(wk_handle* h, const void* d_audio, int32_t dtype, 
           h->ws_used = true;
           return e;
         }
-        if (hipStreamSynchronize(st) == hipSuccess) h->ws_used = false;   // drained: nothing left to wait for
+        if (hipStreamSynchronize(st) == hipSuccess || hipDeviceSynchronize() == hipSuccess) {
+          h->ws_used = false;   // drained: nothing left to wait for
+        } else {
+          h->ws_poisoned = true;   // this call's chunks may still be queued: no later call may reuse the workspace
+        }
         return e;
       }
       ~WsRelease() { (void)release(); }

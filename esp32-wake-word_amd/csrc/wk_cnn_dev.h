@@ -57,7 +57,14 @@ __device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g,
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s8 __attribute__((ext_vector_type(8)));   // one lane's A or B fragment: 8 bf16 bit patterns
 
+#if defined(WK_MFMA_K32) && !defined(WK_ALLOW_K32_DIAG)
+#error "WK_MFMA_K32 corrupts the fused kernel's front-end (DESIGN.md 5.1); diagnostic builds add -DWK_ALLOW_K32_DIAG"
+#endif
 __device__ __forceinline__ f32x4 mfma_bf16(s8 a, s8 b, f32x4 c) {
+#ifdef WK_MFMA_K32   // diagnostic only (tools/debug/xdl_hazard_scan.py)
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                 0);
+#endif
   c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 0, 1, 2, 3),
                                                 __builtin_shufflevector(b, b, 0, 1, 2, 3), c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 4, 5, 6, 7),

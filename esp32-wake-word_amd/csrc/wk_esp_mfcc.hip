@@ -35,6 +35,7 @@
 #include <new>
 #include <vector>
 
+#include "wk_esp_tables.h"
 #include "wk_kernels.h"
 
 struct wk_esp_mfcc {
@@ -49,34 +50,6 @@ struct wk_esp_mfcc {
 };
 
 namespace {
-
-// mfcc.c:133-142 (hz_to_mel takes f = 0 as 1; mel_to_hz uses the base-10 form).
-float esp_hz_to_mel(float f) { return 1127.0f * log1pf((f == 0.0f ? 1.0f : f) / 700.0f); }
-float esp_mel_to_hz(float m) { return 700.0f * (powf(10.0f, m / 2595.0f) - 1.0f); }
-
-// create_mel_filterbank(sr, n_filters, n_fft, 0, -1) (mfcc.c:144-234) as
-// dense rows [n_filters][n_fft / 2 + 1].
-std::vector<float> esp_filterbank(int sr, int n_filters, int n_fft) {
-  const int nb = n_fft / 2 + 1;
-  std::vector<float> fb((size_t)n_filters * nb, 0.0f);
-  const float lo = esp_hz_to_mel(0.0f), hi = esp_hz_to_mel((float)(sr / 2));
-  const float bw = (float)sr / n_fft;
-  std::vector<int> bin(n_filters + 2);
-  for (int i = 0; i < n_filters + 2; ++i) bin[i] = (int)floorf(esp_mel_to_hz(lo + i * (hi - lo) / (n_filters + 1)) / bw);
-  auto clamp = [nb](int v) { return v < 0 ? 0 : (v >= nb ? nb - 1 : v); };
-  for (int f = 0; f < n_filters; ++f) {
-    int l = clamp(bin[f]), c = clamp(bin[f + 1]), r = clamp(bin[f + 2]);
-    if (l >= c) c = l + 1;
-    if (c >= r) r = c + 1;
-    if (r >= nb) r = nb - 1;
-    float* row = fb.data() + (size_t)f * nb;
-    for (int j = l; j <= c; ++j)
-      if (j >= 0 && j < nb) row[j] = (float)(j - l) / (c - l);
-    for (int j = c; j <= r; ++j)   // (r == c at the top of a crowded bank: 0/0, a NaN weight, as in the reference)
-      if (j >= 0 && j < nb) row[j] = (float)(r - j) / (r - c);
-  }
-  return fb;
-}
 
 constexpr int kEspBlock = 256;
 
@@ -184,24 +157,21 @@ wk_status wk_esp_mfcc_create(int32_t sampling_rate, int32_t frame_size, int32_t 
                              int32_t n_mfcc, int32_t esp_dsp_packing, int32_t device, wk_esp_mfcc** out) {
   if (!out) return invalid("wk_esp_mfcc_create: null out");
   *out = nullptr;
-  int lg = 0;
-  while (lg < 31 && (1 << lg) < n_fft) ++lg;
-  if (sampling_rate < 1 || frame_size < 1 || n_fft < 2 || n_fft > 4096 || (1 << lg) != n_fft || n_filters < 1 ||
-      n_filters > 1024 || n_mfcc < 1)
+  const int lg = wk::esp::check_domain(sampling_rate, frame_size, n_fft, n_filters, n_mfcc);
+  if (lg < 0)
     return invalid("wk_esp_mfcc_create: parameters outside mfcc.c's domain (n_fft a power of 2 in [2, 4096], "
                    "1 <= n_filters <= 1024, frame_size, n_mfcc, sampling_rate >= 1)");
   wk_esp_mfcc* m = new (std::nothrow) wk_esp_mfcc;
   if (!m) return WK_ERR_NO_MEMORY;
   *m = wk_esp_mfcc{sampling_rate, frame_size, n_fft, n_filters, n_mfcc, esp_dsp_packing ? 1 : 0, device, lg};
   // window (mfcc.c:118-120: alpha - (1 - alpha) cos(2 pi i / (frame - 1)), float, the angle in double)
-  std::vector<float> win(frame_size);
-  for (int i = 0; i < frame_size; ++i) win[i] = 0.53836f - (1.0f - 0.53836f) * cosf(2.0f * M_PI * i / (frame_size - 1));
+  const std::vector<float> win = wk::esp::window(frame_size);
   std::vector<float2> tw(n_fft / 2);
   for (int k = 0; k < n_fft / 2; ++k)
     tw[k] = make_float2((float)cos(2.0 * M_PI * k / n_fft), (float)-sin(2.0 * M_PI * k / n_fft));
   // sparse mel rows: the span of each row's nonzero (or NaN) weights
   const int nb = n_fft / 2 + 1;
-  const std::vector<float> fb = esp_filterbank(sampling_rate, n_filters, n_fft);
+  const std::vector<float> fb = wk::esp::filterbank(sampling_rate, n_filters, n_fft);
   std::vector<int2> rows(n_filters);
   std::vector<int> rlen(n_filters);
   std::vector<float> fbw;
@@ -218,12 +188,8 @@ wk_status wk_esp_mfcc_create(int32_t sampling_rate, int32_t frame_size, int32_t 
     for (int k = lo; k <= hi; ++k) fbw.push_back(fb[(size_t)f * nb + k]);
   }
   // DCT-II cosines (mfcc.c:26-30 / :44-48: cos of the float-converted double angle) and scales (:33, :57)
-  const int n_dct = n_mfcc < n_filters ? n_mfcc : n_filters;
-  std::vector<float> dct((size_t)n_dct * n_filters), scale(n_dct);
-  for (int k = 0; k < n_dct; ++k) {
-    for (int i = 0; i < n_filters; ++i) dct[(size_t)k * n_filters + i] = cosf(M_PI * k * (2 * i + 1) / (2.0f * n_filters));
-    scale[k] = k == 0 ? sqrtf(1.0f / n_filters) : sqrtf(2.0f / n_filters);
-  }
+  std::vector<float> dct, scale;
+  wk::esp::dct(n_mfcc, n_filters, dct, scale);
   const wk_status s = wk::on_device(device, [&]() -> wk_status {
     hipError_t e;
     if ((e = upload(&m->d_win, win)) != hipSuccess || (e = upload(&m->d_tw, tw)) != hipSuccess ||

@@ -481,7 +481,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
   // now (fused: its buffer goes back to the front-end a whole batch earlier;
   // the double buffer otherwise stalled the front-end ~13 % of the time in fp32).
   auto try_eager = [&](int64_t b) {
-    if (!1 || cw >= NBF || eager_done) return;
+    if (cw >= NBF || eager_done) return;
     const int64_t i = (b + 1) * NBF + cw;
     if (i >= n_mine) return;
     if (src.ready(i)) {

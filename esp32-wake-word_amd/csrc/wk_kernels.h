@@ -8,14 +8,13 @@
 #include <string>
 
 #include "wakeword.h"
+#include "wk_status.h"
 
 namespace wk {
 
-// Error reporting shared by the C-ABI translation units (wk_api.hip, wk_ctc.hip).
-extern thread_local std::string g_last_error;
+// Error reporting shared by the C-ABI translation units (wk_api.hip, wk_ctc.hip;
+// g_last_error, invalid and fail in wk_status.h).
 wk_status hip_fail(hipError_t e, const char* what);
-wk_status invalid(const char* what);
-wk_status fail(wk_status s, const char* what);
 
 // Run `body` with device `dev` current; restore the caller's device.
 template <typename F>

@@ -1,7 +1,8 @@
-// wk_wav.hip -- host-side WAV ingest and waveform augmentation (SURVEY 8(f)
+// wk_wav.cpp -- host-side WAV ingest and waveform augmentation (SURVEY 8(f)
 // item 4): the data formats on the input side of the hot path.  Pure host
-// C++ (no device code): it fills caller buffers -- typically pinned host
-// memory handed to wk_forward's H2D copy.
+// C++ (no device code), compiled into both libwakeword.so and
+// libwakeword_host.so: it fills caller buffers -- typically pinned host
+// memory handed to wk_forward's H2D copy, or the host path's input.
 //
 //   wk_wav_read        esp_wav.cpp:8-139  (RIFF / WAVE / "fmt " header, unknown
 //                      chunks before "data" skipped, PCM16, truncation)
@@ -21,7 +22,7 @@
 #include <vector>
 
 #include "wakeword.h"
-#include "wk_kernels.h"
+#include "wk_status.h"
 
 using wk::fail;
 using wk::invalid;

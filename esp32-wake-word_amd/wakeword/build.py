@@ -20,8 +20,10 @@ REPO = os.path.dirname(ROOT)
 CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(PKG, "libwakeword.so")
+HOST_LIB = os.path.join(PKG, "libwakeword_host.so")      # the host-CPU library (wk_host.cpp, no HIP)
+HOST_SOURCES = ["wk_host.cpp", "wk_wav.cpp"]   # (wk_wav.cpp is host C++ in both libraries)
 OBJDIR = os.path.join(ROOT, "build")
-SOURCES = ["wk_frontend.hip", "wk_fused.hip", "wk_misc.hip", "wk_api.hip", "wk_ctc.hip", "wk_wav.hip", "wk_int8.hip", "wk_esp_mfcc.hip"]
+SOURCES = ["wk_frontend.hip", "wk_fused.hip", "wk_misc.hip", "wk_api.hip", "wk_ctc.hip", "wk_wav.cpp", "wk_int8.hip", "wk_esp_mfcc.hip"]
 LIBS = ["-L/opt/rocm/lib", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]   # rocBLAS: plain GEMMs of the CTC head
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WK_OFFLOAD_ARCH", "gfx950")
@@ -40,15 +42,32 @@ def _compile(src: str, extra) -> str:
     return obj
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _stale(lib: str = LIB) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "wakeword.h"), __file__]
-    return any(os.path.getmtime(d) > t for d in deps)
+    t = os.path.getmtime(lib)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, h) for h in os.listdir(INCLUDE)]
+    return any(os.path.getmtime(d) > t for d in deps + [__file__])
+
+
+def build_host(force: bool = False) -> str:
+    """libwakeword_host.so: the host-CPU path (include/wakeword_host.h), plain
+    g++ -- it links no HIP and is what a caller without a GPU loads."""
+    if not force and not _stale(HOST_LIB):
+        return HOST_LIB
+    cxx = os.environ.get("CXX", "g++")
+    tmp = HOST_LIB + ".tmp"
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", "-I", INCLUDE, "-I", CSRC,
+           *[os.path.join(CSRC, f) for f in HOST_SOURCES], "-Wl,--no-undefined", "-o", tmp]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"host library build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, HOST_LIB)
+    return HOST_LIB
 
 
 def build(force: bool = False, extra=()) -> str:
+    build_host(force)
     if not force and not _stale():
         return LIB
     if shutil.which(HIPCC) is None and not os.path.exists(HIPCC):

@@ -1,4 +1,4 @@
-// Host-only ASan/UBSan harness for the WAV ingest (csrc/wk_wav.hip, the
+// Host-only ASan/UBSan harness for the WAV ingest (csrc/wk_wav.cpp, the
 // replacement of esp_wav.cpp:8-139) -- test infrastructure, built and run by
 // tests/test_sanitizers.py on the CPU (never on the GPU box).
 //

@@ -122,6 +122,16 @@ def test_init_rank_gloo_rehearsal_is_marked_shared():
         assert d.calls == [("gloo", {})]
 
 
+def test_init_rank_multinode_is_not_a_rehearsal():
+    """torchrun over 2 nodes x 8 GPUs: WORLD_SIZE 16 > 8 visible GPUs, but 8
+    ranks per node (LOCAL_WORLD_SIZE), one GPU each -- a real measurement."""
+    for r in (0, 9, 15):
+        env = {"WORLD_SIZE": "16", "RANK": str(r), "LOCAL_RANK": str(r % 8), "LOCAL_WORLD_SIZE": "8"}
+        t, d = _FakeTorch(8), _FakeDist()
+        world, rank, local, shared = bench.init_rank(_args(16, "nccl"), env, t, d)
+        assert (world, rank, local, shared) == (16, r, r % 8, False)
+
+
 def test_single_rank_forms_no_group():
     env = {}
     t, d = _FakeTorch(1), _FakeDist()

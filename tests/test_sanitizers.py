@@ -1,6 +1,6 @@
 """ASan + UBSan over the host C/C++ that reads untrusted input or is the
 checker ("race detection / sanitizers"): the WAV ingest
-(csrc/wk_wav.hip, replacing esp_wav.cpp:8-139) under truncated, corrupted,
+(csrc/wk_wav.cpp, replacing esp_wav.cpp:8-139) under truncated, corrupted,
 odd-chunk and mis-declared files, and the C oracle (oracle/esp_mfcc_oracle.c)
 over its edge parameter sets.  Host-only builds with clang (-fsanitize=
 address,undefined, -fno-sanitize-recover=all: any report fails the run);
@@ -33,7 +33,7 @@ def test_wav_ingest_under_asan_ubsan(tmp_path):
     exe = str(tmp_path / "wav_harness")
     _run([CLANG, "-std=c++17", *SAN, "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-I", os.path.join(REPO, "include"),
           "-I", os.path.join(REPO, "esp32-wake-word_amd", "csrc"), "-x", "c++",
-          os.path.join(REPO, "esp32-wake-word_amd", "csrc", "wk_wav.hip"), "-x", "none",
+          os.path.join(REPO, "esp32-wake-word_amd", "csrc", "wk_wav.cpp"), "-x", "none",
           os.path.join(REPO, "tests", "sanitize", "wav_harness.cpp"), "-o", exe, "-lpthread"])
     wavs = sorted(glob.glob(os.path.join(REPO, "tests", "golden", "wav", "*.wav")))[:3]
     assert wavs
