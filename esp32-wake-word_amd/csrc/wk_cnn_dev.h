@@ -20,6 +20,12 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f32_4x4x1_16b_f32: 16 independent 4 x 4 x 1 blocks, block b = lane>>2
+// (A: lane 4b + i = row i, B: lane 4b + j = column j; D[r] in lane 4b + j = row r, column j).
+__device__ __forceinline__ f32x4 mfma4x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ float swap_adjacent(float v) {  // lane l <- lane l^1
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
 }
@@ -61,9 +67,14 @@ typedef short s8 __attribute__((ext_vector_type(8)));   // one lane's A or B fra
 #error "WK_MFMA_K32 corrupts the fused kernel's front-end (DESIGN.md 5.1); diagnostic builds add -DWK_ALLOW_K32_DIAG"
 #endif
 __device__ __forceinline__ f32x4 mfma_bf16(s8 a, s8 b, f32x4 c) {
-#ifdef WK_MFMA_K32   // diagnostic only (tools/debug/xdl_hazard_scan.py)
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
-                                                 0);
+#ifdef WK_MFMA_K32   // diagnostic only (tools/debug/xdl_hazard_scan.py, k32_repeat.py)
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+#ifdef WK_K32_PAD   // 16 wait states after every K = 32 MFMA, nothing scheduled across them
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+  return c;
 #endif
   c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 0, 1, 2, 3),
                                                 __builtin_shufflevector(b, b, 0, 1, 2, 3), c, 0, 0, 0);

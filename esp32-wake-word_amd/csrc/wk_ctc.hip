@@ -15,9 +15,11 @@
 //   ctc_zscore_kernel     one block per utterance, two-pass mean / unbiased std.
 //   ctc_encoder_kernel    Linear 80->128 as fp32 MFMA tiles of 16 rows, LayerNorm
 //                         by in-register + 16-lane shuffle sums.
-//   GEMMs (input projections of both GRU directions, the output
-//                         layer): plain library GEMMs (rocblas_gemm_ex; fp16
-//                         operands with fp32 accumulation when precision = 1).
+//   ctc_gemm_nt_kernel    the GEMMs that materialise a [rows][N] tensor (the fp32
+//                         parity mode's input projections and output layer, the
+//                         fp16 A/B path's projections): 128 x 128 MFMA block
+//                         tiles over LDS-staged K chunks, fp32 or fp16 operands,
+//                         fp32 accumulate.
 //   ctc_gru_kernel        persistent recurrence: one 768-thread block per
 //                         (16 utterances, direction); W_hh lives in VGPRs as
 //                         fp32 MFMA A fragments (2 of the 24 16-row tiles per
@@ -29,6 +31,7 @@
 //                         persistent, bias in LDS, a row's loads issued a row
 //                         ahead, no exp.
 //   ctc_greedy_kernel     one wave per utterance: drop blanks, collapse repeats.
+#include <float.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -39,7 +42,6 @@
 #include <vector>
 
 #include <hip/hip_fp16.h>
-#include <rocblas/rocblas.h>
 
 #include "wk_cnn_dev.h"
 #include "wk_kernels.h"
@@ -1855,7 +1857,6 @@ void mel_fbank(std::vector<float>& fb) {
 // ---------------------------------------------------------------------------
 struct wk_ctc {
   wk_ctc_config cfg;
-  rocblas_handle blas;
   int n_cu;
   bool f16;             // precision 1: GEMM operands in fp16 (fp32 accumulate); recurrence fp32
   // weights (device)
@@ -1871,6 +1872,11 @@ struct wk_ctc {
   __half* whh16x_pk[2]; // per layer: [2 dir][3 gates][8 waves][4 k-steps][64 lanes][8] (W_hh as 16x16x32 fragments, gate-scaled)
   __half* wih16x_pk[2]; // per layer: [2 dir][3 gates][8 waves][din/32 k-steps][64 lanes][8] (fused-projection GRU, gate-scaled)
   bool gru_gemm;        // fp16 mode: input projections as a separate GEMM (WAKEWORD_CTC_GEMM=1; A/B and checks)
+  // Decision-parity attribution (WAKEWORD_CTC_MIX): 1 = "out32", the fp16
+  // path up to the last GRU layer, then the output layer in fp32 (y1 widened,
+  // fp32 W); 2 = "out16", the fp32 path with the fp16 output kernel (y1 and W
+  // rounded to fp16).  0 (default) = the precision's own output layer.
+  int mix;
   __half* out_w16;
   float* fft_win;       // [400] periodic Hann
   float* fft_tw;        // [20 k1][20 n2] W400^(n2 k1), complex
@@ -1963,7 +1969,6 @@ void free_all(wk_ctc* c) {
                 c->out_w16, c->fft_win, c->fft_tw, c->whh16_pk[0], c->whh16_pk[1],
                 c->wih16x_pk[0], c->wih16x_pk[1], c->whh16x_pk[0], c->whh16x_pk[1], c->melw, c->melws};
   for (void* q : ps) (void)hipFree(q);
-  if (c->blas) rocblas_destroy_handle(c->blas);
 }
 
 template <typename T>
@@ -1979,19 +1984,168 @@ hipError_t upload_f16(__half** d, const float* h, size_t n) {
   return upload(d, t.data(), n);
 }
 
-// Row-major C[M][N] (fp32, or fp16 with c16) = A[M][K] * W[N][K]^T with A, W
-// fp32 or fp16 (fp32 accumulate).  rocBLAS is column-major: C^T = W * A^T.
-wk_status gemm_nt(rocblas_handle h, int64_t M, int64_t N, int64_t K, const void* A, const void* W, void* C, bool f16,
-                  bool c16 = false) {
-  const float one = 1.0f, zero = 0.0f;
-  const rocblas_datatype ab = f16 ? rocblas_datatype_f16_r : rocblas_datatype_f32_r;
-  const rocblas_datatype cd = c16 ? rocblas_datatype_f16_r : rocblas_datatype_f32_r;
-  const rocblas_status s = rocblas_gemm_ex_64(h, rocblas_operation_transpose, rocblas_operation_none, N, M, K, &one, W,
-                                              ab, K, A, ab, K, &zero, C, cd, N, C, cd, N, rocblas_datatype_f32_r,
-                                              rocblas_gemm_algo_standard, 0, 0);
-  return s == rocblas_status_success ? WK_OK : fail(WK_ERR_HIP, "rocblas_gemm_ex failed");
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Plain GEMM C[M][N] = A[M][K] W[N][K]^T, fp32 accumulate, for the paths that
+// materialise a [rows][N] tensor: the fp32 parity mode's input projections (N =
+// 768) and output layer (N = V, ctc.py:146), and the fp16 A/B path's
+// projections (WAKEWORD_CTC_GEMM=1).  fp32 operands on v_mfma_f32_16x16x4_f32
+// (exact fp32 products and sums), fp16 on v_mfma_f32_16x16x16_f16.
+// Block tile 128 rows x 128 columns, 4 waves of 64 x 64 (4 x 4 accumulators
+// of 16 x 16).  K goes in chunks of 64 bytes per row (16 fp32 / 32 fp16): the
+// block stages a chunk of its A rows and W rows in LDS (double-buffered, one
+// barrier per chunk; the next chunk's global loads are in flight during this
+// chunk's MFMAs), and a lane reads its fragments as 16-byte pieces: lane
+// group q = lane >> 4 holds piece q of a row (E = 4 fp32 / 8 fp16 k), and MFMA
+// step s takes element s (fp32) or elements 4s .. 4s + 3 (fp16) of it -- the
+// same k permutation in A and W, so the chunk is complete after its steps.
+// Rows past M and columns past N read a clamped row and are never stored.
+// K is a multiple of the chunk.  LDS rows are 80 bytes (64 + 16 pad): the
+// 16-byte fragment reads of a lane group land on distinct bank windows.
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int kGemmBM = 128, kGemmBN = 128, kGemmPitch = 5;   // LDS row pitch in 16-byte pieces
+
+// Element-wise fp16 <-> fp32 copy (the WAKEWORD_CTC_MIX attribution paths).
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void ctc_convert_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if constexpr (std::is_same<TO, __half>::value) out[i] = __float2half((float)in[i]);
+    else out[i] = (float)in[i];
+  }
 }
 
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void ctc_gemm_nt_kernel(const TI* __restrict__ A, const TI* __restrict__ W,
+                                                          TO* __restrict__ C, int64_t M, int N, int K) {
+  constexpr bool F16 = std::is_same<TI, __half>::value;
+  constexpr int E = 16 / (int)sizeof(TI), KC = 4 * E;
+  __shared__ uint4 As[2][kGemmBM * kGemmPitch], Ws[2][kGemmBN * kGemmPitch];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, q = lane >> 4, wm = wave >> 1, wn = wave & 1;
+  const int64_t r0 = (int64_t)blockIdx.x * kGemmBM;
+  const int c0 = blockIdx.y * kGemmBN;
+  // cooperative staging: thread tid moves pieces p = tid and tid + 256 of each
+  // operand (row p >> 2, piece p & 3 of the chunk)
+  const uint4* ga[2];
+  const uint4* gw[2];
+  int so[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int p = tid + 256 * h, row = p >> 2, pc = p & 3;
+    const int64_t ra = r0 + row < M ? r0 + row : M - 1;
+    const int cw = c0 + row < N ? c0 + row : N - 1;
+    ga[h] = reinterpret_cast<const uint4*>(A + ra * K) + pc;
+    gw[h] = reinterpret_cast<const uint4*>(W + (int64_t)cw * K) + pc;
+    so[h] = row * kGemmPitch + pc;
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int nch = K / KC;
+  uint4 pa[2], pw[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    pa[h] = ga[h][0];
+    pw[h] = gw[h][0];
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    As[0][so[h]] = pa[h];
+    Ws[0][so[h]] = pw[h];
+  }
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nch) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        pa[h] = ga[h][4 * (c + 1)];
+        pw[h] = gw[h][4 * (c + 1)];
+      }
+    }
+    uint4 a[4], w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = As[buf][(64 * wm + 16 * i + li) * kGemmPitch + q];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = Ws[buf][(64 * wn + 16 * j + li) * kGemmPitch + q];
+    if constexpr (F16) {
+      typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint2 au = st ? make_uint2(a[i].z, a[i].w) : make_uint2(a[i].x, a[i].y);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint2 wu = st ? make_uint2(w[j].z, w[j].w) : make_uint2(w[j].x, w[j].y);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4v, au), __builtin_bit_cast(h4v, wu),
+                                                              acc[i][j], 0, 0, 0);
+          }
+        }
+    } else {
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float av = __uint_as_float(st == 0 ? a[i].x : st == 1 ? a[i].y : st == 2 ? a[i].z : a[i].w);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float wv = __uint_as_float(st == 0 ? w[j].x : st == 1 ? w[j].y : st == 2 ? w[j].z : w[j].w);
+            acc[i][j] = mfma4(av, wv, acc[i][j]);
+          }
+        }
+    }
+    if (c + 1 < nch) {   // buffer buf ^ 1 was last read in chunk c - 1, before the barrier below it
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        As[buf ^ 1][so[h]] = pa[h];
+        Ws[buf ^ 1][so[h]] = pw[h];
+      }
+    }
+    __syncthreads();
+  }
+  // D of a 16 x 16 tile: lane holds rows 4q .. 4q + 3, column li
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = c0 + 64 * wn + 16 * j + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = r0 + 64 * wm + 16 * i + 4 * q + r;
+        if (row < M && col < N) {
+          if constexpr (std::is_same<TO, __half>::value) C[row * N + col] = __float2half(acc[i][j][r]);
+          else C[row * N + col] = acc[i][j][r];
+        }
+      }
+    }
+}
+
+// Row-major C[M][N] (fp32, or fp16 with c16) = A[M][K] * W[N][K]^T with A, W
+// fp32 or fp16 (fp32 accumulate), on `st`.
+wk_status gemm_nt(hipStream_t st, int64_t M, int64_t N, int64_t K, const void* A, const void* W, void* C, bool f16,
+                  bool c16 = false) {
+  if (M <= 0) return WK_OK;
+  if (K % (f16 ? 32 : 16) != 0 || N > INT32_MAX || K > INT32_MAX || (M + kGemmBM - 1) / kGemmBM > INT32_MAX)
+    return fail(WK_ERR_UNSUPPORTED, "ctc gemm: K must be a multiple of 16 (fp32) / 32 (fp16)");
+  const dim3 g((unsigned)((M + kGemmBM - 1) / kGemmBM), (unsigned)((N + kGemmBN - 1) / kGemmBN));
+  if (f16 && c16)
+    hipLaunchKernelGGL((ctc_gemm_nt_kernel<__half, __half>), g, dim3(256), 0, st, (const __half*)A, (const __half*)W,
+                       (__half*)C, M, (int)N, (int)K);
+  else if (f16)
+    hipLaunchKernelGGL((ctc_gemm_nt_kernel<__half, float>), g, dim3(256), 0, st, (const __half*)A, (const __half*)W,
+                       (float*)C, M, (int)N, (int)K);
+  else
+    hipLaunchKernelGGL((ctc_gemm_nt_kernel<float, float>), g, dim3(256), 0, st, (const float*)A, (const float*)W,
+                       (float*)C, M, (int)N, (int)K);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WK_OK : hip_fail(e, "ctc gemm launch");
+}
 
 }  // namespace
 
@@ -2012,12 +2166,10 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     c->f16 = cfg->precision == 1;
     const char* gg = getenv("WAKEWORD_CTC_GEMM");
     c->gru_gemm = gg && gg[0] == '1';
+    const char* mx = getenv("WAKEWORD_CTC_MIX");
+    c->mix = mx ? (strcmp(mx, "out32") == 0 ? 1 : strcmp(mx, "out16") == 0 ? 2 : 0) : 0;
     hipDeviceProp_t prop;
     c->n_cu = hipGetDeviceProperties(&prop, cfg->device) == hipSuccess ? prop.multiProcessorCount : 256;
-    if (rocblas_create_handle(&c->blas) != rocblas_status_success) {
-      free(c);
-      return fail(WK_ERR_HIP, "rocblas_create_handle failed");
-    }
     const int H = kH, V = cfg->vocab;
     const float* p = w;
     auto take = [&](size_t n) { const float* q = p; p += n; return q; };
@@ -2087,7 +2239,7 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     }
     const float* ow = take((size_t)V * 2 * H);
     if (e == hipSuccess) e = upload(&c->out_w, ow, (size_t)V * 2 * H);
-    if (e == hipSuccess && c->f16) e = upload_f16(&c->out_w16, ow, (size_t)V * 2 * H);
+    if (e == hipSuccess && (c->f16 || c->mix == 2)) e = upload_f16(&c->out_w16, ow, (size_t)V * 2 * H);
     if (e == hipSuccess) e = upload(&c->out_b, take(V), V);
     if (e == hipSuccess) {
       const std::vector<float> z((size_t)V, 0.0f);
@@ -2250,8 +2402,9 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
       if ((!f16 && (e = hipMalloc(&c->x0, sizeof(float) * rows * H)) != hipSuccess) ||
           ((!f16 || c->gru_gemm) && (e = hipMalloc(&c->gi, sizeof(float) * rows * 6 * H)) != hipSuccess) ||
           (!f16 && (e = hipMalloc(&c->y0, sizeof(float) * rows * 2 * H)) != hipSuccess) ||
-          (!f16 && (e = hipMalloc(&c->y1, sizeof(float) * rows * 2 * H)) != hipSuccess) ||
-          (!f16 && (e = hipMalloc(&c->logits, sizeof(float) * rows * V)) != hipSuccess) ||
+          ((!f16 || c->mix == 1) && (e = hipMalloc(&c->y1, sizeof(float) * rows * 2 * H)) != hipSuccess) ||
+          ((!f16 || c->mix == 1) && (e = hipMalloc(&c->logits, sizeof(float) * rows * V)) != hipSuccess) ||
+          (!f16 && c->mix == 2 && (e = hipMalloc(&c->y1h, sizeof(__half) * rows * 2 * H)) != hipSuccess) ||
           (e = hipMalloc(&c->best, sizeof(int) * rows)) != hipSuccess ||
           (f16 && (e = hipMalloc(&c->x0h, sizeof(__half) * rows * H)) != hipSuccess) ||
           (f16 && (e = hipMalloc(&c->y0h, sizeof(__half) * rows * 2 * H)) != hipSuccess) ||
@@ -2262,7 +2415,6 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
       }
       c->ws_rows = rows;
     }
-    if (rocblas_set_stream(c->blas, st) != rocblas_status_success) return fail(WK_ERR_HIP, "rocblas_set_stream");
     c->last_batch = batch;
     c->last_T = T;
     const int enc_grid = (int)((rows + 63) / 64 < 2 * c->n_cu ? (rows + 63) / 64 : 2 * c->n_cu);
@@ -2302,8 +2454,8 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
         continue;
       }
       s = timed(c, WK_CTC_STAGE_PROJ0 + 2 * l, st, [&]() -> wk_status {
-        return f16 ? gemm_nt(c->blas, rows, 6 * H, din, in16, c->wih16[l], c->gi, true, true)   // fp16 gates
-                   : gemm_nt(c->blas, rows, 6 * H, din, in, c->wih[l], c->gi, false);
+        return f16 ? gemm_nt(st, rows, 6 * H, din, in16, c->wih16[l], c->gi, true, true)   // fp16 gates
+                   : gemm_nt(st, rows, 6 * H, din, in, c->wih[l], c->gi, false);
       });
       if (s != WK_OK) return s;
       const dim3 gg((unsigned)((batch + kGruBatch - 1) / kGruBatch), 2);
@@ -2320,7 +2472,24 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
       in = ys[l];
       in16 = ys16[l];
     }
-    if (f16) {
+    if (f16 && c->mix == 1) {   // attribution: the fp16 path's y1, widened, through the fp32 output layer
+      if (d_log_probs) return fail(WK_ERR_UNSUPPORTED, "WAKEWORD_CTC_MIX=out32 decodes only (no log-probs)");
+      hipLaunchKernelGGL((ctc_convert_kernel<__half, float>), dim3(2 * c->n_cu), dim3(256), 0, st, c->y1h, c->y1,
+                         rows * 2 * H);
+      in = c->y1;
+    } else if (!f16 && c->mix == 2) {   // attribution: the fp32 path's y1, rounded, through the fp16 output kernel
+      hipLaunchKernelGGL((ctc_convert_kernel<float, __half>), dim3(2 * c->n_cu), dim3(256), 0, st, c->y1, c->y1h,
+                         rows * 2 * H);
+      const dim3 og((unsigned)((rows + out_rows(false) - 1) / out_rows(false)));
+      const bool keyed = V <= 16 * 256;
+      hipLaunchKernelGGL((keyed ? ctc_out_argmax16_kernel<false, true> : ctc_out_argmax16_kernel<false, false>), og,
+                         dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, (__half*)nullptr, c->best);
+      hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
+                         d_tokens, d_lengths, 0);
+      e = hipGetLastError();
+      return e == hipSuccess ? WK_OK : hip_fail(e, "wk_ctc_forward launch");
+    }
+    if (f16 && c->mix != 1) {
       // fused output layer + argmax; fp16 logits are written only for log_softmax
       const dim3 og((unsigned)((rows + out_rows(d_log_probs != nullptr) - 1) / out_rows(d_log_probs != nullptr)));
       s = timed(c, WK_CTC_STAGE_OUTPUT, st, [&]() -> wk_status {
@@ -2350,7 +2519,7 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
     const bool arg_only = !d_log_probs && V % Vec<float>::N == 0 && V / Vec<float>::N <= 64 * kArgChunks && V <= 16384;
     const unsigned ag = (unsigned)((rows + 3) / 4 < 8 * c->n_cu ? (rows + 3) / 4 : 8 * c->n_cu);
     s = timed(c, WK_CTC_STAGE_OUTPUT, st, [&]() -> wk_status {
-      wk_status g = gemm_nt(c->blas, rows, V, 2 * H, c->y1, c->out_w, c->logits, false);
+      wk_status g = gemm_nt(st, rows, V, 2 * H, in, c->out_w, c->logits, false);
       if (g != WK_OK) return g;
       if (arg_only)
         hipLaunchKernelGGL(ctc_argmax_only_kernel<float>, dim3(ag), dim3(256), V * sizeof(float), st, c->logits,
@@ -2363,7 +2532,7 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
     if (s == WK_OK)
       s = timed(c, WK_CTC_STAGE_DECODE, st, [&]() -> wk_status {
         hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
-                           d_tokens, d_lengths);
+                           d_tokens, d_lengths, f16 ? 1 : 0);   // (fp16 rows are time-major)
         return WK_OK;
       });
     if (s != WK_OK) return s;

@@ -49,8 +49,9 @@ constexpr int kFusedBlock = 1024;    // 8 front-end + 8 CNN waves
 // group of a B-fragment read (ds_read_b128 fp32 / ds_read_b64 bf16) and of the
 // pooled stores land on distinct banks.
 constexpr int kGOff = (kFeLds + 3) & ~3;            // pooled features [128][4] (16-byte aligned carve below)
-constexpr int kFcpOff = kGOff + 128 * NBF;          // classifier.0 partials [2][64][4]
-constexpr int kL1Off = kFcpOff + 2 * 64 * NBF;      // second log-mel buffer [40][64] (first: kLOff)
+constexpr int kFcpOff = kGOff + 128 * NBF;          // classifier.0 partials [8 k-slices][4 clips][64 o]
+constexpr int kFcpSize = 8 * NBF * 64;
+constexpr int kL1Off = kFcpOff + kFcpSize;          // second log-mel buffer [40][64] (first: kLOff)
 static_assert(kLOff % 4 == 0 && kL1Off % 4 == 0, "log-mel buffers are read with ds_read_b128");
 constexpr int kCtrlOff = kL1Off + kLSize;           // control words
 constexpr int kImgOff = (kCtrlOff + 16 + 3) & ~3;   // 16-byte aligned
@@ -99,7 +100,7 @@ static_assert(kPOff + kPSize <= kGOff && kLOff + kLSize <= kPOff && kImgEnd <= k
 // Inside the window, the front-end writes the second log-mel buffer and the
 // control words; the CNN role's writes (pooled features, classifier partials,
 // every precision's image set) sit in ranges that miss it.
-static_assert(kGOff + 128 * NBF <= kFcpOff && kFcpOff + 2 * 64 * NBF <= kL1Off && kL1Off + kLSize <= kCtrlOff &&
+static_assert(kGOff + 128 * NBF <= kFcpOff && kFcpOff + kFcpSize <= kL1Off && kL1Off + kLSize <= kCtrlOff &&
                   kCtrlOff + 16 <= kImgOff,
               "pooled features | partials | log-mel buffer 1 | control words, in that order, disjoint");
 static_assert(kF2End <= kImgEnd && kB2Off + NBF * I2_TP * I2_CIP / 2 <= kImgEnd &&
@@ -489,21 +490,21 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       eager_done = true;
     }
   };
-  // ReLU -> classifier.2 (64 -> 1) of batch bb from the classifier.0 partials:
-  // lane = (o group q = lane>>2, clip = lane&3).  Run by one wave, deferred to
-  // just after the next batch's first barrier (one barrier per batch fewer).
+  // ReLU -> classifier.2 (64 -> 1) of batch bb from the classifier.0 partials
+  // (one per CNN wave's k-slice): lane = (o group q = lane>>2, clip = lane&3),
+  // one 16-byte read per slice.  Run by one wave, deferred to just after the
+  // next batch's first barrier (one barrier per batch fewer).
   auto fc2 = [&](int64_t bb) {
     if (cw != 0) return;
     int ln = lane;
     asm volatile("" : "+v"(ln));
     const int cl = ln & (NBF - 1), q = ln >> 2;
+    f32x4 h = *reinterpret_cast<const f32x4*>(FCP + cl * 64 + 4 * q);
+#pragma unroll
+    for (int w = 1; w < 8; ++w) h += *reinterpret_cast<const f32x4*>(FCP + (w * NBF + cl) * 64 + 4 * q);
     float acc = 0.0f;
 #pragma unroll
-    for (int i2 = 0; i2 < 4; ++i2) {
-      const int o = 4 * q + i2;
-      const float h = fmaxf(FCP[o * NBF + cl] + FCP[64 * NBF + o * NBF + cl], 0.0f);
-      acc = __builtin_fmaf(buf_load(rs, 16 * q, 4 * (kPkF2 + i2)), h, acc);
-    }
+    for (int i2 = 0; i2 < 4; ++i2) acc = __builtin_fmaf(buf_load(rs, 16 * q, 4 * (kPkF2 + i2)), fmaxf(h[i2], 0.0f), acc);
     acc += __shfl_xor(acc, 4, 64);
     acc += __shfl_xor(acc, 8, 64);
     acc += __shfl_xor(acc, 16, 64);
@@ -654,28 +655,26 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
     float wf1[16];
     {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) wf1[s] = buf_load(rs, lv, 4 * (kPkF1 + ((cw & 3) * 32 + 16 * (cw >> 2) + s) * 64));
+      for (int s = 0; s < 16; ++s) wf1[s] = buf_load(rs, lv, 4 * (kPkF1 + (cw * 16 + s) * 64));
     }
     WK_STAMP(5);
     role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);
     try_eager(b);
     WK_STAMP(6);
 
-    // classifier.0 (128 -> 64): o tile (cw&3), k half (cw>>2); columns >= NBF are don't-care.
+    // classifier.0 (128 -> 64) on v_mfma_f32_4x4x1_16b_f32: 16 blocks of 4 o x
+    // 4 clips, block b = lane>>2 taking o = 4b .. 4b + 3 (A: lane = o, B: lane
+    // & 3 = clip), so every column is a real clip (the 16x16x4 form used 4 of its
+    // 16); wave cw takes k = 16 cw .. 16 cw + 15, and its partial
+    // [o = 4(lane>>2) + r][clip lane&3] leaves as one 16-byte store.
     {
       int ln = lane;
       asm volatile("" : "+v"(ln));   // addresses recomputed here rather than kept live (and spilled)
-      const int li = ln & 15, lk = ln >> 4;
       f32x4 acc = {0, 0, 0, 0};
-      const int kh = cw >> 2;
+      const float* g = Gp + 16 * cw * NBF + (ln & (NBF - 1));
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        acc = mfma4(wf1[s], Gp[(64 * kh + 4 * s + lk) * NBF + (li & (NBF - 1))], acc);
-      }
-      if (li < NBF) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) FCP[kh * 64 * NBF + (16 * (cw & 3) + 4 * lk + r) * NBF + li] = acc[r];
-      }
+      for (int s = 0; s < 16; ++s) acc = mfma4x4(wf1[s], g[s * NBF], acc);
+      *reinterpret_cast<f32x4*>(FCP + (cw * NBF + (ln & (NBF - 1))) * 64 + 4 * (ln >> 2)) = acc;
     }
     // No barrier here: classifier.2 of this batch reads the partials after the
     // next batch's first barrier (below), which already orders them; the

@@ -80,12 +80,13 @@ constexpr int kNumWeights = kOffF2 + 64;        // 40224
 //   conv ([clip][t][ci] images): step s = 4 (tap * CB + cb) + j, lane group
 //     q = l>>4 feeds ci = 16 cb + 4 q + j at that tap (Cin padded to 16);
 //     taps 0 and 2 are g0, g2, tap 1 the Winograd tap G1 = (g0 + g1 + g2) / 2.
-//   classifier.0: k = 4s + q.
+//   classifier.0 (v_mfma_f32_4x4x1_16b_f32, 16 blocks): wave w, step s feeds
+//     k = 16 w + s; lane l is the output row o = l.
 constexpr int kPkW1 = 0;                        // [2 tiles][12 s][64]
 constexpr int kPkW2 = kPkW1 + 2 * 12 * 64;      // [4][24][64]
 constexpr int kPkW3 = kPkW2 + 4 * 24 * 64;      // [8][48][64]
-constexpr int kPkF1 = kPkW3 + 8 * 48 * 64;      // [4 o-tiles][32 s][64]  (k = 4s + lane>>4)
-constexpr int kPkF2 = kPkF1 + 4 * 32 * 64;      // [64]
+constexpr int kPkF1 = kPkW3 + 8 * 48 * 64;      // [8 waves][16 s][64 o]  (k = 16 w + s)
+constexpr int kPkF2 = kPkF1 + 8 * 16 * 64;      // [64]
 constexpr int kNumPacked = kPkF2 + 64;
 
 // bf16 variant (WK_PREC_BF16 / BF16X3, v_mfma_f32_16x16x32_bf16): per 16-row
@@ -154,12 +155,9 @@ inline void pack_fragments(const float* w, float* pk) {
   conv_blocked(kPkW1, 2, 13, 16, kOffW1);
   conv_blocked(kPkW2, 4, 32, 32, kOffW2);
   conv_blocked(kPkW3, 8, 64, 64, kOffW3);
-  for (int t = 0; t < 4; ++t)
-    for (int s = 0; s < 32; ++s)
-      for (int l = 0; l < 64; ++l) {
-        const int o = 16 * t + (l & 15), c = 4 * s + (l >> 4);
-        pk[kPkF1 + (t * 32 + s) * 64 + l] = w[kOffF1 + o * 128 + c];
-      }
+  for (int wv = 0; wv < 8; ++wv)
+    for (int s = 0; s < 16; ++s)
+      for (int o = 0; o < 64; ++o) pk[kPkF1 + (wv * 16 + s) * 64 + o] = w[kOffF1 + o * 128 + 16 * wv + s];
   for (int o = 0; o < 64; ++o) pk[kPkF2 + o] = w[kOffF2 + o];
 }
 

@@ -24,7 +24,7 @@ HOST_LIB = os.path.join(PKG, "libwakeword_host.so")      # the host-CPU library 
 HOST_SOURCES = ["wk_host.cpp", "wk_wav.cpp"]   # (wk_wav.cpp is host C++ in both libraries)
 OBJDIR = os.path.join(ROOT, "build")
 SOURCES = ["wk_frontend.hip", "wk_fused.hip", "wk_misc.hip", "wk_api.hip", "wk_ctc.hip", "wk_wav.cpp", "wk_int8.hip", "wk_esp_mfcc.hip"]
-LIBS = ["-L/opt/rocm/lib", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]   # rocBLAS: plain GEMMs of the CTC head
+LIBS = ["-Wl,-rpath,/opt/rocm/lib"]   # HIP runtime only: every GEMM is a hand-written kernel (no rocBLAS)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WK_OFFLOAD_ARCH", "gfx950")
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-fno-signed-zeros", "-ffp-contract=fast", "-fno-slp-vectorize",

@@ -8,5 +8,5 @@ FL="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -fno-signed-zeros -ffp-contract=f
 mkdir -p build/diag
 for f in wk_frontend wk_fused wk_misc wk_api wk_ctc wk_int8 wk_esp_mfcc; do $HIPCC $FL -c csrc/$f.hip -o build/diag/$f.o & done; wait
 $HIPCC $FL -c csrc/wk_wav.cpp -o build/diag/wk_wav.o || { echo "compile of wk_wav failed"; exit 1; }
-$HIPCC --offload-arch=gfx950 -shared -fPIC build/diag/*.o -L/opt/rocm/lib -lrocblas -Wl,-rpath,/opt/rocm/lib -o build/diag/libwakeword_diag.so
+$HIPCC --offload-arch=gfx950 -shared -fPIC build/diag/*.o -Wl,-rpath,/opt/rocm/lib -o build/diag/libwakeword_diag.so
 echo "$R/esp32-wake-word_amd/build/diag/libwakeword_diag.so"
