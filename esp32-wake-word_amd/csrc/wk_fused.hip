@@ -40,6 +40,17 @@ __device__ unsigned long long g_wk_stamps[16][16];
 #define WK_SP_ARG
 #endif
 
+#ifdef WK_DIAG_PROW
+// Diagnostic builds only (-DWK_DIAG_PROW, tools/debug/prow_probe.py; the K = 32
+// question of DESIGN.md 5.1): the power rows of each workgroup's first
+// kProwClips clips, three snapshots [3][grid * kProwClips][64][257]: A = what
+// each front-end lane wrote (read back right after its round), B = the rows
+// after the clip's role barrier, just before the mel reads them, C = the same
+// rows after the mel.
+__device__ float* g_prow_dbg;
+constexpr int kProwClips = 4;
+#endif
+
 
 constexpr int NBF = 4;               // clips per CNN batch
 constexpr int kFusedBlock = 1024;    // 8 front-end + 8 CNN waves
@@ -300,9 +311,28 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       WK_STAMP(1);
       float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
       fe_rest<true>(a, j, row, row + (fl & 1), tb, w0, tws, 0, pf_part WK_SP_ARG);
+#ifdef WK_DIAG_PROW
+      if (i < kProwClips && fl < kNFramesB && g_prow_dbg) {   // snapshot A: this lane's bins as it wrote them
+        float* dA = g_prow_dbg + ((size_t)(blockIdx.x * kProwClips + i) * 64 + fl) * 257;
+        for (int k2 = 0; k2 < 8; ++k2) {
+          dA[j + 16 * k2] = row[j + 16 * k2];
+          dA[256 - j - 16 * k2] = row[256 - j - 16 * k2];
+        }
+        if (j == 0) dA[128] = row[128];
+      }
+#endif
     }
     role_sync<kPrioFe>(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
     WK_STAMP(7);
+#ifdef WK_DIAG_PROW
+    auto prow_snap = [&](int k) {   // snapshots B (k = 1) and C (k = 2): wave w copies frames w, w + 8, ...
+      if (i >= kProwClips || !g_prow_dbg) return;
+      float* d = g_prow_dbg + (size_t)k * gridDim.x * kProwClips * 64 * 257;
+      for (int f = wave; f < kNFramesB; f += 8)
+        for (int b = lane; b < 257; b += 64) d[((size_t)(blockIdx.x * kProwClips + i) * 64 + f) * 257 + b] = P[f * kPRow + b];
+    };
+    prow_snap(1);
+#endif
     if (i >= 2 && !(diag & 1)) spin_until_all8<kPrioFe>(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
     WK_STAMP(10);
     {
@@ -315,6 +345,9 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       mel_dispatch<true>(wave, smem + prow, (i & 1 ? L1 : L) + lane);
     }
     WK_STAMP(8);
+#ifdef WK_DIAG_PROW
+    prow_snap(2);
+#endif
     signal_add(ctrl, kCtrlLReady, lane);
     // Split barrier: arrive now, wait before this wave next writes a power
     // row (round 0 of clip i+1), after its stage 0 and prefetch.
@@ -854,6 +887,12 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_cnn_fused_kernel(const floa
 }  // namespace
 
 
+
+#ifdef WK_DIAG_PROW
+extern "C" int wk_debug_prow_buffer(void* d) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_prow_dbg), &d, sizeof(d)) != hipSuccess;
+}
+#endif
 
 #ifdef WK_DIAG
 extern "C" int wk_debug_stamps(unsigned long long* host_out, int reset) {

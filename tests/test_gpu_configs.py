@@ -235,6 +235,13 @@ def test_config5_decision_parity(precision, out_scale, mix, monkeypatch):
         ntok += len(ref_seqs[j])
     frame_agree = float((pred[idx] == ref_lp.argmax(-1)).float().mean())
     match, mean_dist = exact / len(idx), dist / len(idx)
+    # the oracle's top-2 log-prob margin at every frame whose decision differs (a near-tie or not)
+    flip = (pred[idx] != ref_lp.argmax(-1))
+    top2 = ref_lp.topk(2, dim=-1).values
+    margins = (top2[..., 0] - top2[..., 1])[flip]
+    print(f"\nconfig5 flipped frames: {int(flip.sum())}, oracle top-2 margins at them: max "
+          f"{float(margins.max()) if margins.numel() else 0.0:.2e}, median "
+          f"{float(margins.median()) if margins.numel() else 0.0:.2e}")
     print(f"\nconfig5 decisions ({precision}{'+' + mix if mix else ''}, out_scale {out_scale}): exact-sequence match "
           f"{match:.4f} ({exact}/{len(idx)}), mean edit distance {mean_dist:.3f} tokens per utterance "
           f"(oracle mean length {ntok / len(idx):.1f}), frame-argmax agreement {frame_agree:.5f}")
