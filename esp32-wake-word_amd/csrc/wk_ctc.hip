@@ -1552,6 +1552,26 @@ __device__ __forceinline__ float out_tag(float x, unsigned sel, unsigned tag) {
   const unsigned u = __builtin_bit_cast(unsigned, x);
   return __builtin_bit_cast(float, __builtin_amdgcn_perm(u, u, sel) ^ tag);
 }
+// Runner-up tracking (KEYED): the second largest of {m, k0, k1} is their
+// median; the row's running second maximum is max(m2, med3(m, k0, k1)).
+__device__ __forceinline__ float out_med3(float a, float b, float c) {
+  float r;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float out_max(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// Near-tie re-scoring (decision parity): a row whose top-2 tagged
+// logits are closer than this is re-decided between those two columns in fp32
+// (ctc_rescore_kernel).  The fp16 operands move a logit by ~3e-4 rms here
+// (256 products of fp16-rounded weights); the margin test is generous.
+__device__ __forceinline__ bool out_near_tie(float m1, float m2) {
+  return m1 - m2 < 4e-3f + 2e-3f * fabsf(m1);
+}
+
 // The column block (4 tile + cf) of a tagged value.
 __device__ __forceinline__ int out_untag(float m) {
   const unsigned u = __builtin_bit_cast(unsigned, m);
@@ -1562,7 +1582,8 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
                                                                           const __half* __restrict__ w,
                                                                           const float* __restrict__ bias, int64_t rows,
                                                                           int V, __half* __restrict__ logits,
-                                                                          int* __restrict__ best) {
+                                                                          int* __restrict__ best,
+                                                                          int* __restrict__ best2) {
   constexpr int kOutRF = out_rf(LOGITS), kOutRows = out_rows(LOGITS);
   __shared__ __attribute__((aligned(1024))) _Float16 bt[kOutNB][kOutBN * kOutPitch];   // (EARLYDMA: row addresses XOR the chunk)
   // the tile's bias, staged with its W rows (an L2 load per column in the
@@ -1629,14 +1650,14 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   dma_w(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  float mx[kOutRF][4];
+  float mx[kOutRF][4], mx2[kOutRF][4];   // (mx2: KEYED runner-up)
   int ix[kOutRF][4];
   unsigned ksel;   // (KEYED) the v_perm_b32 selector of out_tag, in a VGPR (VOP3 takes no literal)
   asm("v_mov_b32 %0, 0x03020109" : "=v"(ksel));
 #pragma unroll
   for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { mx[rf][i] = -INFINITY; ix[rf][i] = 0; }
+    for (int i = 0; i < 4; ++i) { mx[rf][i] = -INFINITY; mx2[rf][i] = -INFINITY; ix[rf][i] = 0; }
   // Skew: the second half of the waves (4-7, each the partner of
   // a first-half wave on the same SIMD) runs one tile behind in its epilogue:
   // per tile it finishes tile nt - 1's argmax first, then issues tile nt's
@@ -1677,7 +1698,9 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
                 x0 = v - 16 < V ? x0 : -FLT_MAX;
                 x1 = v < V ? x1 : -FLT_MAX;
               }
-              mx[rf][i] = out_max3(mx[rf][i], out_tag(x0, ksel, tag + 1), out_tag(x1, ksel, tag));
+              const float t0 = out_tag(x0, ksel, tag + 1), t1 = out_tag(x1, ksel, tag), m = mx[rf][i];
+              mx2[rf][i] = out_max(mx2[rf][i], out_med3(m, t0, t1));
+              mx[rf][i] = out_max3(m, t0, t1);
             }
         }
       } else if (decltype(full)::value || v < V) {
@@ -1741,15 +1764,60 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     for (int i = 0; i < 4; ++i) {
       float m = mx[rf][i];
       int k = KEYED ? 16 * out_untag(m) + li : ix[rf][i];
+      float m2 = mx2[rf][i];   // (KEYED) runner-up and its column
+      int k2 = KEYED ? 16 * out_untag(m2) + li : -1;
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
         const float om = __shfl_xor(m, o, 64);
         const int ok = __shfl_xor(k, o, 64);
+        if (KEYED) {
+          const float om2 = __shfl_xor(m2, o, 64);
+          const int ok2 = __shfl_xor(k2, o, 64);
+          // the merged runner-up: the loser of the two maxima, or the larger runner-up
+          const bool other_wins = om > m || (om == m && ok < k);
+          const float lm = other_wins ? m : om;
+          const int lk = other_wins ? k : ok;
+          const bool r_other = om2 > m2 || (om2 == m2 && ok2 < k2);
+          const float rm = r_other ? om2 : m2;
+          const int rk = r_other ? ok2 : k2;
+          const bool use_loser = lm > rm || (lm == rm && lk < rk);
+          m2 = use_loser ? lm : rm;
+          k2 = use_loser ? lk : rk;
+        }
         if (om > m || (om == m && ok < k)) { m = om; k = ok; }
       }
       const int64_t r = row0 + 16 * rf + 4 * lg + i;
-      if (li == 0 && r < rows) best[r] = k;
+      if (li == 0 && r < rows) {
+        best[r] = k;
+        best2[r] = KEYED && m2 > -INFINITY && out_near_tie(m, m2) ? k2 : -1;
+      }
     }
+}
+
+// Near-tie re-scoring after ctc_out_argmax16_kernel (fp16 mode, V <= 4096):
+// a row whose top-2 logits came within out_near_tie of each other is decided
+// between those two columns again with fp32 weights (y is the fp16 GRU output,
+// widened exactly): bias + sum_k y[k] W[c][k] as an fp32 fmaf chain, the
+// larger wins, an exact tie keeps the smaller column (torch.argmax).  Rows
+// with best2 < 0 keep their fp16 decision.  One thread per row.
+__global__ __launch_bounds__(256) void ctc_rescore_kernel(const __half* __restrict__ y, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, int64_t rows,
+                                                          int* __restrict__ best, const int* __restrict__ best2) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  const int c2 = best2[r];
+  if (c2 < 0) return;
+  const int c1 = best[r];
+  const __half* yr = y + r * (2 * kH);
+  const float* w1 = w + (int64_t)c1 * (2 * kH);
+  const float* w2 = w + (int64_t)c2 * (2 * kH);
+  float s1 = bias[c1], s2 = bias[c2];
+  for (int k = 0; k < 2 * kH; ++k) {
+    const float yk = __half2float(yr[k]);
+    s1 = __builtin_fmaf(yk, w1[k], s1);
+    s2 = __builtin_fmaf(yk, w2[k], s2);
+  }
+  if (s2 > s1 || (s2 == s1 && c2 < c1)) best[r] = c2;
 }
 
 // Window starts of ctc_logmel_fft2_kernel's straight-line filterbank.  A tap
@@ -1877,6 +1945,7 @@ struct wk_ctc {
   // fp32 W); 2 = "out16", the fp32 path with the fp16 output kernel (y1 and W
   // rounded to fp16).  0 (default) = the precision's own output layer.
   int mix;
+  int rescore;          // fp16 output layer: near-tie rows re-decided in fp32 (default; WAKEWORD_CTC_RESCORE=0 off, A/B)
   __half* out_w16;
   float* fft_win;       // [400] periodic Hann
   float* fft_tw;        // [20 k1][20 n2] W400^(n2 k1), complex
@@ -1887,6 +1956,7 @@ struct wk_ctc {
   float *x0, *gi, *y0, *y1, *logits;
   __half *x0h, *y0h, *y1h, *logits16;
   int* best;
+  int* best2;           // fp16 mode: the runner-up column of near-tie rows (else -1), for ctc_rescore_kernel
   float* tr_feats;      // wk_ctc_transcribe: [rows][80] features (raw in fp16 mode), pass partials, per-utterance z-score
   float4* tr_part;
   float2* tr_zs;
@@ -1912,11 +1982,11 @@ int64_t ctc_num_weights(const wk_ctc_config* c) {
 }
 
 void free_ws(wk_ctc* c) {   // (wk_ctc_forward's workspace; the transcribe buffers go in free_all)
-  void* ps[] = {c->x0, c->gi, c->y0, c->y1, c->logits, c->best, c->x0h, c->y0h, c->y1h, c->logits16};
+  void* ps[] = {c->x0, c->gi, c->y0, c->y1, c->logits, c->best, c->best2, c->x0h, c->y0h, c->y1h, c->logits16};
   for (void* q : ps) (void)hipFree(q);
   c->x0 = c->gi = c->y0 = c->y1 = c->logits = nullptr;
   c->x0h = c->y0h = c->y1h = c->logits16 = nullptr;
-  c->best = nullptr;
+  c->best = c->best2 = nullptr;
   c->ws_rows = 0;
 }
 
@@ -2168,6 +2238,8 @@ wk_status wk_ctc_create(const wk_ctc_config* cfg, const float* w, wk_ctc** out) 
     c->gru_gemm = gg && gg[0] == '1';
     const char* mx = getenv("WAKEWORD_CTC_MIX");
     c->mix = mx ? (strcmp(mx, "out32") == 0 ? 1 : strcmp(mx, "out16") == 0 ? 2 : 0) : 0;
+    const char* rs = getenv("WAKEWORD_CTC_RESCORE");
+    c->rescore = !(rs && rs[0] == '0');
     hipDeviceProp_t prop;
     c->n_cu = hipGetDeviceProperties(&prop, cfg->device) == hipSuccess ? prop.multiProcessorCount : 256;
     const int H = kH, V = cfg->vocab;
@@ -2406,6 +2478,7 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
           ((!f16 || c->mix == 1) && (e = hipMalloc(&c->logits, sizeof(float) * rows * V)) != hipSuccess) ||
           (!f16 && c->mix == 2 && (e = hipMalloc(&c->y1h, sizeof(__half) * rows * 2 * H)) != hipSuccess) ||
           (e = hipMalloc(&c->best, sizeof(int) * rows)) != hipSuccess ||
+          (e = hipMalloc(&c->best2, sizeof(int) * rows)) != hipSuccess ||
           (f16 && (e = hipMalloc(&c->x0h, sizeof(__half) * rows * H)) != hipSuccess) ||
           (f16 && (e = hipMalloc(&c->y0h, sizeof(__half) * rows * 2 * H)) != hipSuccess) ||
           (f16 && (e = hipMalloc(&c->y1h, sizeof(__half) * rows * 2 * H)) != hipSuccess) ||
@@ -2483,7 +2556,11 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
       const dim3 og((unsigned)((rows + out_rows(false) - 1) / out_rows(false)));
       const bool keyed = V <= 16 * 256;
       hipLaunchKernelGGL((keyed ? ctc_out_argmax16_kernel<false, true> : ctc_out_argmax16_kernel<false, false>), og,
-                         dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, (__half*)nullptr, c->best);
+                         dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, (__half*)nullptr, c->best,
+                         c->best2);
+      if (keyed && c->rescore)
+        hipLaunchKernelGGL(ctc_rescore_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, c->y1h, c->out_w,
+                           c->out_b, rows, c->best, c->best2);
       hipLaunchKernelGGL(ctc_greedy_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, c->best, batch, T,
                          d_tokens, d_lengths, 0);
       e = hipGetLastError();
@@ -2496,14 +2573,18 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
         const bool keyed = 1 && V <= 16 * 256;   // the tag holds kOutCF tile + cf in 8 bits
         if (d_log_probs) {
           hipLaunchKernelGGL((keyed ? ctc_out_argmax16_kernel<true, true> : ctc_out_argmax16_kernel<true, false>), og,
-                             dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, c->logits16, c->best);
+                             dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, c->logits16, c->best,
+                             c->best2);
           hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st,
                              c->logits16, c->zero_b, rows, V, d_log_probs, (int*)nullptr, (int)batch, T);   // bias already in
         } else {
           hipLaunchKernelGGL((keyed ? ctc_out_argmax16_kernel<false, true> : ctc_out_argmax16_kernel<false, false>), og,
                              dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, (__half*)nullptr,
-                             c->best);
+                             c->best, c->best2);
         }
+        if (keyed && c->rescore)   // near-tie rows decided again in fp32 (tokens independent of log-probs: both variants)
+          hipLaunchKernelGGL(ctc_rescore_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, c->y1h,
+                             c->out_w, c->out_b, rows, c->best, c->best2);
         return WK_OK;
       });
       if (s == WK_OK)

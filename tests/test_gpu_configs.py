@@ -197,11 +197,11 @@ def _edit_distance(a, b):
 # an fp32 output layer, "out16" = the fp32 path with the fp16 output kernel.
 CTC_DECISION_BOUNDS = {("fp16", 4.0, ""): (0.60, 0.80, 0.997), ("fp16", 1.0, ""): (0.60, 0.80, 0.997),
                        ("fp32", 4.0, ""): (0.60, 0.80, 0.997),
-                       ("fp16", 4.0, "out32"): (0.50, 1.00, 0.997), ("fp32", 4.0, "out16"): (0.50, 1.00, 0.997)}
+                       ("fp16", 4.0, "norescore"): (0.50, 1.00, 0.997), ("fp16", 1.0, "norescore"): (0.50, 1.00, 0.997),
+                       ("fp16", 4.0, "out32"): (0.50, 1.00, 0.997), ("fp32", 4.0, "out16+norescore"): (0.50, 1.00, 0.997)}
 
 
-@pytest.mark.parametrize("precision,out_scale,mix", [("fp16", 4.0, ""), ("fp16", 1.0, ""), ("fp32", 4.0, ""),
-                                                     ("fp16", 4.0, "out32"), ("fp32", 4.0, "out16")])
+@pytest.mark.parametrize("precision,out_scale,mix", list(CTC_DECISION_BOUNDS))
 def test_config5_decision_parity(precision, out_scale, mix, monkeypatch):
     """Config 5's product output is the token sequence (decode_predictions,
     ctc.py:453-471).  For 64 utterances spread over the B = 4096 batch, the
@@ -212,8 +212,11 @@ def test_config5_decision_parity(precision, out_scale, mix, monkeypatch):
     import torch
     import wakeword
     from oracle import wk_ctc_oracle as CO
-    if mix:
-        monkeypatch.setenv("WAKEWORD_CTC_MIX", mix)
+    for part in mix.split("+") if mix else []:
+        if part == "norescore":
+            monkeypatch.setenv("WAKEWORD_CTC_RESCORE", "0")
+        else:
+            monkeypatch.setenv("WAKEWORD_CTC_MIX", part)
     B, V, n = 4096, 4000, 48000
     T = 1 + n // 160
     m = CO.make_model(V, seed=0, out_scale=out_scale)
