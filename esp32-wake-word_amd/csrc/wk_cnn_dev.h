@@ -16,6 +16,17 @@ namespace wk {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifdef WK_DIAG_PROW
+// Diagnostic builds only (the K = 32 question): every epilogue
+// store's element index is checked against its image (4 clips x rows x pitch)
+// or the pooled-feature array; an index outside sets this word
+// (wk_debug_epi_bad in wk_fused.hip reads it).
+static __device__ unsigned g_epi_bad;
+#define WK_EPI_GUARD(idx, lim) do { if ((unsigned)(idx) >= (unsigned)(lim)) g_epi_bad = 1u; } while (0)
+#else
+#define WK_EPI_GUARD(idx, lim) do {} while (0)
+#endif
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -44,7 +55,10 @@ __device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g,
     s += dpp<0x4E>(s);
     s += dpp<0x141>(s);
     s += dpp<0x140>(s);
-    if (tt == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s * (1.0f / 7.0f);
+    if (tt == 0) {
+      WK_EPI_GUARD((co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip, 128 * GSTRIDE);
+      g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s * (1.0f / 7.0f);
+    }
   }
 }
 
@@ -137,6 +151,7 @@ __device__ __forceinline__ void epi_pool_bf(const f32x4& acc, uint16_t* __restri
     uint2 pkd;
     pkd.x = bf16_bits(v[0]) | (bf16_bits(v[1]) << 16);
     pkd.y = bf16_bits(v[2]) | (bf16_bits(v[3]) << 16);
+    WK_EPI_GUARD((clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4) + 3, 4 * TP_N * CIP_N);
     *reinterpret_cast<uint2*>(next + (clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4)) = pkd;
   }
 }
@@ -185,6 +200,7 @@ __device__ __forceinline__ void epi_pool_bf3(const f32x4& acc, uint16_t* __restr
     l[r] = bf16_bits(v - __uint_as_float(h[r] << 16));
   }
   if (!(lane & 1) && tp < TN) {
+    WK_EPI_GUARD((clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4) + LO + 3, 4 * TP_N * CIP_N);
     uint16_t* p = next + (clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4);
     *reinterpret_cast<uint2*>(p) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
     *reinterpret_cast<uint2*>(p + LO) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
@@ -248,9 +264,11 @@ __device__ __forceinline__ void epi_wino_pool(const f32x4 (&m)[4], float* __rest
     const float y0 = m[0][r] + m[1][r] + m[2][r], y1 = m[1][r] - m[2][r] - m[3][r];
     v[r] = fmaxf(fmaxf(y0, y1), 0.0f);
   }
-  if (p < TN)
+  if (p < TN) {
+    WK_EPI_GUARD((clip * TP_N + 1 + p) * CIP_N + co0 + 4 * (lane >> 4) + 3, 4 * TP_N * CIP_N);
     *reinterpret_cast<float4*>(next + (clip * TP_N + 1 + p) * CIP_N + co0 + 4 * (lane >> 4)) =
         make_float4(v[0], v[1], v[2], v[3]);
+  }
 }
 
 // conv3's tile holds two clips (columns 0-7: clip ca, 8-15: clip ca + 1; 8
@@ -266,7 +284,10 @@ __device__ __forceinline__ void epi_wino_gap(const f32x4 (&m)[4], float* __restr
     s += dpp<0xB1>(s);    // 8-lane sum: quad_perm xor 1, xor 2, row_half_mirror
     s += dpp<0x4E>(s);
     s += dpp<0x141>(s);
-    if (p == 0) g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s * (1.0f / 7.0f);
+    if (p == 0) {
+      WK_EPI_GUARD((co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip, 128 * GSTRIDE);
+      g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s * (1.0f / 7.0f);
+    }
   }
 }
 

@@ -1601,7 +1601,15 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       uint4 v = make_uint4(0, 0, 0, 0);
+#ifdef WK_OUT_Y_NT   // A/B: the once-read y rows non-temporal, so they do not evict W tiles from L2
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      if (r < rows) {
+        const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(y + r * kOutK + 32 * st + 8 * lg));
+        v = make_uint4(t[0], t[1], t[2], t[3]);
+      }
+#else
       if (r < rows) v = *reinterpret_cast<const uint4*>(y + r * kOutK + 32 * st + 8 * lg);
+#endif
       a[rf][st] = __builtin_bit_cast(h8, v);
     }
   }

@@ -48,6 +48,9 @@ __device__ unsigned long long g_wk_stamps[16][16];
 // after the clip's role barrier, just before the mel reads them, C = the same
 // rows after the mel.
 __device__ float* g_prow_dbg;
+// ... and the same clips' log-mel images [2][grid * kProwClips][40][64]: D = as
+// the front-end's mel left them, E = as the CNN wave's DCT is about to read them.
+__device__ float* g_lmel_dbg;
 constexpr int kProwClips = 4;
 #endif
 
@@ -332,6 +335,13 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
         for (int b = lane; b < 257; b += 64) d[((size_t)(blockIdx.x * kProwClips + i) * 64 + f) * 257 + b] = P[f * kPRow + b];
     };
     prow_snap(1);
+    if (i >= 1 && i - 1 < kProwClips && g_lmel_dbg) {
+      // snapshot D of clip i - 1: its log-mel image as the front-end's mel left it (complete: every wave has
+      // passed this clip's barrier since; the buffer is next written by clip i + 1's mel), wave w rows w, w + 8, ...
+      const float* lb = ((i - 1) & 1 ? L1 : L);
+      float* d = g_lmel_dbg + (size_t)(blockIdx.x * kProwClips + i - 1) * 40 * 64;
+      for (int m = wave; m < 40; m += 8) d[m * 64 + lane] = lb[m * WK_LSTRIDE + lane];
+    }
 #endif
     if (i >= 2 && !(diag & 1)) spin_until_all8<kPrioFe>(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
     WK_STAMP(10);
@@ -757,6 +767,13 @@ struct LogmelSrc {
     if (!(diag & 2)) spin_until<0>(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
   }
   __device__ __forceinline__ void load(int64_t i, int slot) const {
+#ifdef WK_DIAG_PROW
+    if (i < kProwClips && g_lmel_dbg) {   // snapshot E: the whole image as this CNN wave is about to read it
+      const float* lb = smem + (i & 1 ? kL1Off : kLOff);
+      float* d = g_lmel_dbg + ((size_t)gridDim.x * kProwClips + clip_base * kProwClips + i) * 40 * 64;
+      for (int e = lane; e < 40 * 64; e += 64) d[e] = lb[(e >> 6) * WK_LSTRIDE + (e & 63)];
+    }
+#endif
     float* fo = FEATS ? feats_out + (clip_base + clip_step * i) * (13 * kNFramesB) : nullptr;
     dct_cmvn_clip<CM>(smem + (i & 1 ? kL1Off : kLOff), slot, smem + kF0Off,
                       reinterpret_cast<uint16_t*>(smem + kB0Off), reinterpret_cast<uint16_t*>(smem + kX0Off), fo,
@@ -891,6 +908,15 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_cnn_fused_kernel(const floa
 #ifdef WK_DIAG_PROW
 extern "C" int wk_debug_prow_buffer(void* d) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_prow_dbg), &d, sizeof(d)) != hipSuccess;
+}
+extern "C" int wk_debug_lmel_buffer(void* d) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_lmel_dbg), &d, sizeof(d)) != hipSuccess;
+}
+// Reads (and with reset clears) the epilogue bounds-check word of wk_cnn_dev.h.
+extern "C" int wk_debug_epi_bad(unsigned* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_epi_bad), sizeof(unsigned)) != hipSuccess) return 1;
+  const unsigned zero = 0;
+  return reset && hipMemcpyToSymbol(HIP_SYMBOL(g_epi_bad), &zero, sizeof(zero)) != hipSuccess;
 }
 #endif
 

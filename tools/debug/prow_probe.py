@@ -29,19 +29,30 @@ prec = sys.argv[1] if len(sys.argv) > 1 else "bf16"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 L = _lib.lib()
 L.wk_debug_prow_buffer.argtypes = [C.c_void_p]
+L.wk_debug_lmel_buffer.argtypes = [C.c_void_p]
+L.wk_debug_epi_bad.argtypes = [C.c_void_p, C.c_int]
 m = wakeword.load_onnx(os.path.join(R, "tests", "golden", "xiaoa.onnx"), precision=prec)
 x = wakeword.synth_clips(777, 0, 65536, device=0)
 grid = 256   # (the fused launch's grid on a 256-CU MI355X: min(batch, n_cu))
 buf = torch.full((3, grid * 4, 64, 257), float("nan"), dtype=torch.float32, device="cuda:0")
+lbuf = torch.full((2, grid * 4, 40, 64), float("nan"), dtype=torch.float32, device="cuda:0")
 assert L.wk_debug_prow_buffer(C.c_void_p(buf.data_ptr())) == 0
-snaps, logits = [], []
+assert L.wk_debug_lmel_buffer(C.c_void_p(lbuf.data_ptr())) == 0
+bad = C.c_uint(0)
+L.wk_debug_epi_bad(C.byref(bad), 1)
+snaps, lsnaps, logits = [], [], []
 for _ in range(n):
     buf.fill_(float("nan"))
+    lbuf.fill_(float("nan"))
     lg, _f = m.detect(x, return_features=True)
     torch.cuda.synchronize()
     snaps.append(buf[:, :, :63].cpu().numpy().copy())
+    lsnaps.append(lbuf[:, :, :, :63].cpu().numpy().copy())
     logits.append(lg.reshape(-1).cpu().numpy().copy())
 L.wk_debug_prow_buffer(None)
+L.wk_debug_lmel_buffer(None)
+L.wk_debug_epi_bad(C.byref(bad), 1)
+print(f"epilogue bounds check over {n} launches: {'an epilogue store left its image' if bad.value else 'every store inside its image'}")
 m.check_device_errors()
 tag = os.path.basename(os.path.dirname(os.environ.get("WAKEWORD_LIB", "prod")))
 for r, s in enumerate(snaps):
@@ -55,6 +66,11 @@ for r, s in enumerate(snaps):
     clips_lg = int((logits[r] != logits[0]).sum())
     msg = (f"{tag} {prec} launch {r}: rows with A!=B {rows_ab}, B!=C {rows_bc}; rows whose A differs from launch 0 "
            f"{rows_a0} (of {a.shape[0] * a.shape[1]}); clips whose logit differs from launch 0 {clips_lg} (of 65536)")
+    d, e = lsnaps[r]
+    de = ~((d == e) | (np.isnan(d) & np.isnan(e)))
+    dl = ~((d == lsnaps[0][0]) | (np.isnan(d) & np.isnan(lsnaps[0][0])))
+    msg += (f"; log-mel images: D!=E (hand-off) {int(de.any(axis=(1, 2)).sum())} of {d.shape[0]}, "
+            f"D differs from launch 0 {int(dl.any(axis=(1, 2)).sum())}")
     print(msg, flush=True)
     if rows_ab:
         cl, fr = np.nonzero(ab.any(axis=2))
