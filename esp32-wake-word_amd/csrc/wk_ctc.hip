@@ -2095,9 +2095,29 @@ __global__ __launch_bounds__(256) void ctc_convert_kernel(const TI* __restrict__
   }
 }
 
-template <typename TI, typename TO>
+// ARGMAX (fp32 decode, no log-probs): C is not written; each row's first
+// argmax of (A W^T)[row] + bias over the block's columns goes to keys[row] by a
+// 64-bit atomicMax on {order-preserving float bits, ~column} (the larger logit
+// wins, an equal logit keeps the smaller column, as torch.argmax), so the
+// [rows][V] fp32 logits never exist (19.7 GB written and read back at config
+// 5 before).  keys must be zeroed first; ctc_keys_to_best_kernel decodes them.
+__device__ __forceinline__ unsigned long long argmax_key(float v, int col) {
+  unsigned u = __float_as_uint(v);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)col);
+}
+
+__global__ __launch_bounds__(256) void ctc_keys_to_best_kernel(const unsigned long long* __restrict__ keys,
+                                                               int64_t rows, int* __restrict__ best) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r < rows) best[r] = (int)(0xFFFFFFFFu - (unsigned)(keys[r] & 0xFFFFFFFFull));
+}
+
+template <typename TI, typename TO, bool ARGMAX = false>
 __global__ __launch_bounds__(256) void ctc_gemm_nt_kernel(const TI* __restrict__ A, const TI* __restrict__ W,
-                                                          TO* __restrict__ C, int64_t M, int N, int K) {
+                                                          TO* __restrict__ C, int64_t M, int N, int K,
+                                                          const float* __restrict__ bias = nullptr,
+                                                          unsigned long long* __restrict__ keys = nullptr) {
   constexpr bool F16 = std::is_same<TI, __half>::value;
   constexpr int E = 16 / (int)sizeof(TI), KC = 4 * E;
   __shared__ uint4 As[2][kGemmBM * kGemmPitch], Ws[2][kGemmBN * kGemmPitch];
@@ -2187,6 +2207,36 @@ __global__ __launch_bounds__(256) void ctc_gemm_nt_kernel(const TI* __restrict__
     }
     __syncthreads();
   }
+  if constexpr (ARGMAX) {
+    float bj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = c0 + 64 * wn + 16 * j + li;
+      bj[j] = col < N ? bias[col] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float bv = -INFINITY;
+        int bc = 0x7FFFFFFF;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // this lane's columns, increasing
+          const int col = c0 + 64 * wn + 16 * j + li;
+          const float v = acc[i][j][r] + bj[j];
+          if (col < N && v > bv) { bv = v; bc = col; }
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {   // the 16 column lanes of the row: first maximum
+          const float ov = __shfl_xor(bv, o, 64);
+          const int oc = __shfl_xor(bc, o, 64);
+          if (ov > bv || (ov == bv && oc < bc)) { bv = ov; bc = oc; }
+        }
+        const int64_t row = r0 + 64 * wm + 16 * i + 4 * q + r;
+        if (li == 0 && row < M && bc < N) atomicMax(keys + row, argmax_key(bv, bc));
+      }
+    return;
+  }
   // D of a 16 x 16 tile: lane holds rows 4q .. 4q + 3, column li
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -2223,6 +2273,23 @@ wk_status gemm_nt(hipStream_t st, int64_t M, int64_t N, int64_t K, const void* A
                        (float*)C, M, (int)N, (int)K);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? WK_OK : hip_fail(e, "ctc gemm launch");
+}
+
+// fp32 best[row] = first argmax of A[M][K] W[N][K]^T + bias (K % 16 == 0),
+// with keys [M] as scratch: zero, GEMM + atomic argmax, decode.
+wk_status gemm_argmax(hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A, const float* W, const float* bias,
+                      unsigned long long* keys, int* best) {
+  if (M <= 0) return WK_OK;
+  if (K % 16 != 0 || N > INT32_MAX || K > INT32_MAX || (M + kGemmBM - 1) / kGemmBM > INT32_MAX)
+    return fail(WK_ERR_UNSUPPORTED, "ctc gemm: K must be a multiple of 16");
+  hipError_t e = hipMemsetAsync(keys, 0, sizeof(unsigned long long) * M, st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+  const dim3 g((unsigned)((M + kGemmBM - 1) / kGemmBM), (unsigned)((N + kGemmBN - 1) / kGemmBN));
+  hipLaunchKernelGGL((ctc_gemm_nt_kernel<float, float, true>), g, dim3(256), 0, st, A, W, (float*)nullptr, M, (int)N,
+                     (int)K, bias, keys);
+  hipLaunchKernelGGL(ctc_keys_to_best_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, keys, M, best);
+  e = hipGetLastError();
+  return e == hipSuccess ? WK_OK : hip_fail(e, "ctc gemm-argmax launch");
 }
 
 }  // namespace
@@ -2608,6 +2675,9 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
     const bool arg_only = !d_log_probs && V % Vec<float>::N == 0 && V / Vec<float>::N <= 64 * kArgChunks && V <= 16384;
     const unsigned ag = (unsigned)((rows + 3) / 4 < 8 * c->n_cu ? (rows + 3) / 4 : 8 * c->n_cu);
     s = timed(c, WK_CTC_STAGE_OUTPUT, st, [&]() -> wk_status {
+      if (!d_log_probs)   // decode only: the argmax inside the GEMM, no [rows][V] logits (c->logits: the keys)
+        return gemm_argmax(st, rows, V, 2 * H, in, c->out_w, c->out_b, reinterpret_cast<unsigned long long*>(c->logits),
+                           c->best);
       wk_status g = gemm_nt(st, rows, V, 2 * H, in, c->out_w, c->logits, false);
       if (g != WK_OK) return g;
       if (arg_only)
