@@ -1601,15 +1601,14 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       uint4 v = make_uint4(0, 0, 0, 0);
-#ifdef WK_OUT_Y_NT   // A/B: the once-read y rows non-temporal, so they do not evict W tiles from L2
+      // Non-temporal: the once-read y rows do not evict the W tiles every
+      // workgroup re-reads from L2 (PMC: 851 -> 681 MB per launch against
+      // 638 MB algorithmic, same time; profiles/r05c_*_ctc_hbm_traffic.json).
       typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
       if (r < rows) {
         const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(y + r * kOutK + 32 * st + 8 * lg));
         v = make_uint4(t[0], t[1], t[2], t[3]);
       }
-#else
-      if (r < rows) v = *reinterpret_cast<const uint4*>(y + r * kOutK + 32 * st + 8 * lg);
-#endif
       a[rf][st] = __builtin_bit_cast(h8, v);
     }
   }
@@ -2079,12 +2078,15 @@ hipError_t upload_f16(__half** d, const float* h, size_t n) {
 // step s takes element s (fp32) or elements 4s .. 4s + 3 (fp16) of it -- the
 // same k permutation in A and W, so the chunk is complete after its steps.
 // Rows past M and columns past N read a clamped row and are never stored.
-// K is a multiple of the chunk.  LDS rows are 80 bytes (64 + 16 pad): the
-// 16-byte fragment reads of a lane group land on distinct bank windows.
+// K is a multiple of the chunk.  LDS rows are 64 bytes with their four 16-byte
+// pieces swizzled (gemm_piece): the fragment reads are bank-conflict-free.
 // ---------------------------------------------------------------------------
 namespace {
 
-constexpr int kGemmBM = 128, kGemmBN = 128, kGemmPitch = 5;   // LDS row pitch in 16-byte pieces
+constexpr int kGemmBM = 128, kGemmBN = 128, kGemmPitch = 4;   // LDS row pitch in 16-byte pieces (swizzled, below)
+// piece q of LDS row n sits at q ^ ((n >> 1) & 3): each 16-lane group of a
+// fragment ds_read_b128 (rows li, pieces q) then covers all 64 banks (brute-forced).
+__device__ __forceinline__ int gemm_piece(int n, int q) { return q ^ ((n >> 1) & 3); }
 
 // Element-wise fp16 <-> fp32 copy (the WAKEWORD_CTC_MIX attribution paths).
 template <typename TI, typename TO>
@@ -2137,7 +2139,7 @@ __global__ __launch_bounds__(256) void ctc_gemm_nt_kernel(const TI* __restrict__
     const int cw = c0 + row < N ? c0 + row : N - 1;
     ga[h] = reinterpret_cast<const uint4*>(A + ra * K) + pc;
     gw[h] = reinterpret_cast<const uint4*>(W + (int64_t)cw * K) + pc;
-    so[h] = row * kGemmPitch + pc;
+    so[h] = row * kGemmPitch + gemm_piece(row, pc);
   }
   f32x4 acc[4][4];
 #pragma unroll
@@ -2159,18 +2161,20 @@ __global__ __launch_bounds__(256) void ctc_gemm_nt_kernel(const TI* __restrict__
   __syncthreads();
   for (int c = 0; c < nch; ++c) {
     const int buf = c & 1;
-    if (c + 1 < nch) {
+    {   // next chunk's pieces (the last chunk re-loads itself: unconditional loads keep pa / pw in
+        // registers -- under a branch the compiler staged them through scratch and waited at once)
+      const int cn = c + 1 < nch ? c + 1 : c;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        pa[h] = ga[h][4 * (c + 1)];
-        pw[h] = gw[h][4 * (c + 1)];
+        pa[h] = ga[h][4 * cn];
+        pw[h] = gw[h][4 * cn];
       }
     }
     uint4 a[4], w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = As[buf][(64 * wm + 16 * i + li) * kGemmPitch + q];
+    for (int i = 0; i < 4; ++i) a[i] = As[buf][(64 * wm + 16 * i + li) * kGemmPitch + gemm_piece(li, q)];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = Ws[buf][(64 * wn + 16 * j + li) * kGemmPitch + q];
+    for (int j = 0; j < 4; ++j) w[j] = Ws[buf][(64 * wn + 16 * j + li) * kGemmPitch + gemm_piece(li, q)];
     if constexpr (F16) {
       typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 #pragma unroll

@@ -51,7 +51,10 @@ __device__ float* g_prow_dbg;
 // ... and the same clips' log-mel images [2][grid * kProwClips][40][64]: D = as
 // the front-end's mel left them, E = as the CNN wave's DCT is about to read them.
 __device__ float* g_lmel_dbg;
-constexpr int kProwClips = 4;
+#ifndef WK_PROW_CLIPS
+#define WK_PROW_CLIPS 32
+#endif
+constexpr int kProwClips = WK_PROW_CLIPS;
 #endif
 
 

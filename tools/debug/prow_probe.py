@@ -4,7 +4,8 @@ question), from a library built with -DWK_DIAG_PROW (tools/debug/build_variant.s
 not a test.
 
 For each of `n` full-size launches (65,536 clips, precision bf16 by default)
-the kernel records, for the first 4 clips of every workgroup, A = the power
+the kernel records, for the first P = 32 clips of every workgroup (clip
+b + 256 i of workgroup b, i < P; -DWK_PROW_CLIPS), A = the power
 bins each front-end lane wrote (read back right after its round), B = the
 rows just before the mel, C = the rows after the mel.  Printed:
   * within each launch, the (clip, frame) rows where A != B or B != C: the
@@ -34,8 +35,11 @@ L.wk_debug_epi_bad.argtypes = [C.c_void_p, C.c_int]
 m = wakeword.load_onnx(os.path.join(R, "tests", "golden", "xiaoa.onnx"), precision=prec)
 x = wakeword.synth_clips(777, 0, 65536, device=0)
 grid = 256   # (the fused launch's grid on a 256-CU MI355X: min(batch, n_cu))
-buf = torch.full((3, grid * 4, 64, 257), float("nan"), dtype=torch.float32, device="cuda:0")
-lbuf = torch.full((2, grid * 4, 40, 64), float("nan"), dtype=torch.float32, device="cuda:0")
+P = int(os.environ.get("WK_PROW_CLIPS", "32"))
+buf = torch.full((3, grid * P, 64, 257), float("nan"), dtype=torch.float32, device="cuda:0")
+# slot s = b * P + i  <->  global clip b + grid * i
+slot_clip = np.array([(s_ // P) + grid * (s_ % P) for s_ in range(grid * P)])
+lbuf = torch.full((2, grid * P, 40, 64), float("nan"), dtype=torch.float32, device="cuda:0")
 assert L.wk_debug_prow_buffer(C.c_void_p(buf.data_ptr())) == 0
 assert L.wk_debug_lmel_buffer(C.c_void_p(lbuf.data_ptr())) == 0
 bad = C.c_uint(0)
@@ -66,11 +70,17 @@ for r, s in enumerate(snaps):
     clips_lg = int((logits[r] != logits[0]).sum())
     msg = (f"{tag} {prec} launch {r}: rows with A!=B {rows_ab}, B!=C {rows_bc}; rows whose A differs from launch 0 "
            f"{rows_a0} (of {a.shape[0] * a.shape[1]}); clips whose logit differs from launch 0 {clips_lg} (of 65536)")
+    diff_clips = logits[r] != logits[0]
+    mon = diff_clips[slot_clip]                     # monitored slots whose logit differs
+    a_rows = da.any(axis=2).any(axis=1)             # slots whose power rows (A) differ from launch 0
+    msg += (f"; monitored clips {len(slot_clip)}, of them logit differs {int(mon.sum())}, "
+            f"power rows (A) differ {int(a_rows.sum())}, both {int((mon & a_rows).sum())}")
     d, e = lsnaps[r]
     de = ~((d == e) | (np.isnan(d) & np.isnan(e)))
     dl = ~((d == lsnaps[0][0]) | (np.isnan(d) & np.isnan(lsnaps[0][0])))
     msg += (f"; log-mel images: D!=E (hand-off) {int(de.any(axis=(1, 2)).sum())} of {d.shape[0]}, "
-            f"D differs from launch 0 {int(dl.any(axis=(1, 2)).sum())}")
+            f"D differs from launch 0 {int(dl.any(axis=(1, 2)).sum())} (of them logit differs "
+            f"{int((dl.any(axis=(1, 2)) & mon).sum())})")
     print(msg, flush=True)
     if rows_ab:
         cl, fr = np.nonzero(ab.any(axis=2))
