@@ -320,10 +320,24 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
       // bound_ctrl off: lane 0 has no source and keeps `old` = its own
       // partner register -- no lane select.
       f2 zq;
+#ifdef WK_SPLIT_BPERM   // diagnostic (the K = 32 question): the partner by ds_bpermute, no DPP
+      {
+        const int src = ((int)__lane_id() & ~15) | ((16 - j) & 15);
+        const float px = __shfl(sv.x, src, 64), py = __shfl(sv.y, src, 64);
+        zq.x = j == 0 ? own.x : px;
+        zq.y = j == 0 ? own.y : py;
+      }
+#else
+#ifdef WK_SPLIT_DPP_PAD   // diagnostic: 5 extra wait states ahead of the partner's DPP moves
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 4" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       zq.x = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.x), __float_as_int(dpp<0x140>(sv.x)),
                                                         0x111, 0xF, 0xF, false));
       zq.y = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), __float_as_int(dpp<0x140>(sv.y)),
                                                         0x111, 0xF, 0xF, false));
+#endif
       S[t] = fma2(zq, f2{1.0f, -1.0f}, zk);
       D[t] = fma2(zq, f2{-1.0f, 1.0f}, zk);
     }
