@@ -2649,7 +2649,7 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
       // fused output layer + argmax; fp16 logits are written only for log_softmax
       const dim3 og((unsigned)((rows + out_rows(d_log_probs != nullptr) - 1) / out_rows(d_log_probs != nullptr)));
       s = timed(c, WK_CTC_STAGE_OUTPUT, st, [&]() -> wk_status {
-        const bool keyed = 1 && V <= 16 * 256;   // the tag holds kOutCF tile + cf in 8 bits
+        const bool keyed = V <= 16 * 256;   // the tag holds kOutCF tile + cf in 8 bits
         if (d_log_probs) {
           hipLaunchKernelGGL((keyed ? ctc_out_argmax16_kernel<true, true> : ctc_out_argmax16_kernel<true, false>), og,
                              dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, c->logits16, c->best,
