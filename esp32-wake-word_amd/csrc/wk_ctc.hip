@@ -143,12 +143,20 @@ struct CtcFft2Lds {
   f2 w[kF2Waves][kF2Pairs * 20 * kA2Pitch];   // per wave: A, then the exchange, then the power rows
 };
 
+// Passes (6 rows each) are dealt to the waves in contiguous ranges of R
+// (wave W takes passes [W R, W R + R)), so a wave walks its rows in order: the
+// (utterance, frame) of its rows advance by addition, with one division per
+// range rather than per pass.
+//
 // STATS (wk_ctc_transcribe, fp16 mode, T >= 6): the features stay un-normalised
-// and each pass also leaves part[ps] = {S0, Q0, S1, Q1}: the sums of (x - K) and
-// (x - K)^2 over its rows' log-mel values x, split between the utterance of the
-// pass's first row (0) and the next one (1), with K = ln(1e-8) the floor of x
-// (so a silent utterance sums to exactly 0).  ctc_zstats_kernel folds them into
-// each utterance's mean and 1/std, which the encoder applies as it loads.
+// and each wave also leaves, per utterance its range touches, the sums of
+// (x - K) and (x - K)^2 over that utterance's log-mel values x in its rows, with
+// K = ln(1e-8) the floor of x (so a silent utterance sums to exactly 0): lanes
+// keep running sums while the utterance lasts and reduce them across the wave
+// only when it changes (2-3 times per range instead of once per pass).  Slot
+// part[W MS + j] holds the range's j-th utterance; ctc_zstats_kernel folds the
+// slots into each utterance's mean and 1/std, which the encoder applies as it
+// loads.
 __device__ __forceinline__ float row16_sum(float v) {   // every lane: the sum over its 16-lane row (DPP)
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
@@ -165,7 +173,8 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
                                                                             const float* __restrict__ melw,
                                                                             const int* __restrict__ melws,
                                                                             float* __restrict__ feats,
-                                                                            float4* __restrict__ part) {
+                                                                            int64_t R, int MS,
+                                                                            float2* __restrict__ part) {
   __shared__ CtcFft2Lds L;
   constexpr int NT = kF2Waves * 64;
   for (int i = threadIdx.x; i < kNfft; i += NT) L.win[i] = win_g[i];
@@ -179,7 +188,8 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
 #define LM_W(p, i, val) (*(vlf2*)((p) + (i)) = (val))
   constexpr int kRowsPerPass = 2 * kF2Pairs;
   const int64_t passes = (rows + kRowsPerPass - 1) / kRowsPerPass;
-  const int64_t pstep = (int64_t)gridDim.x * kF2Waves;
+  const int64_t wid = (int64_t)blockIdx.x * kF2Waves + wv;
+  const int64_t p_beg = wid * R, p_end = p_beg + R < passes ? p_beg + R : passes;
   const int nv_min = n_valid < n_pad ? n_valid : n_pad;
   // The lane's 20 samples x[20 n1 + q] of one frame (row) of pass ps_; idle
   // lanes and rows past the end read utterance 0's first samples (nothing
@@ -203,19 +213,30 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
       }
     }
   };
-  // both frames of the lane group's pair: one division for frame a, frame b is
-  // the next row (t + 1, or frame 0 of the next utterance)
-  int ta_next = 0;
-  auto load_pair = [&](int64_t ps_, float (&ra_)[20], float (&rb_)[20]) {
-    const int64_t row = ps_ * kRowsPerPass + 2 * g;
-    const bool live_a = g < kF2Pairs && ps_ < passes && row < rows;
+  // The pass to load next: its first row (utterance lb, frame lt; wave-
+  // uniform) advances by 6 per pass.  Frame a of the lane group's pair is row
+  // 2 g after it, frame b the next row (t + 1, or frame 0 of the next utterance).
+  int64_t lrow = p_beg * kRowsPerPass;
+  int lb = (int)((unsigned)(lrow < rows ? lrow : 0) / (unsigned)T);   // rows < 2^31 (host check)
+  int lt = (int)(lrow < rows ? lrow : 0) - lb * T;
+  auto load_pair = [&](bool pass_live, float (&ra_)[20], float (&rb_)[20]) {
+    const int64_t row = lrow + 2 * g;
+    const bool live_a = g < kF2Pairs && pass_live && row < rows;
     const bool live_b = live_a && row + 1 < rows;
-    const int rr = live_a ? (int)row : 0;   // rows < 2^31 (host check)
-    const int ba = (int)((unsigned)rr / (unsigned)T), ta = rr - ba * T;
-    ta_next = __builtin_amdgcn_readfirstlane(ta);   // lane 0: the pass's first row (STATS)
+    int ba = lb, ta = lt + 2 * g;
+    while (ta >= T) {   // (once at most for T >= 5)
+      ta -= T;
+      ++ba;
+    }
     const bool wrap = ta + 1 == T;
     load_one(live_a, ba, ta, ra_);
     load_one(live_b, wrap ? ba + 1 : ba, wrap ? 0 : ta + 1, rb_);
+    lrow += kRowsPerPass;
+    lt += kRowsPerPass;
+    while (lt >= T) {
+      lt -= T;
+      ++lb;
+    }
   };
   // the lane's mel windows: mel `lane` (kMelW1 taps from bin ws1) and half
   // `lane & 1` of mel 64 + lane / 2 (kMelW2 taps from ws2; lanes >= 32: zero weights)
@@ -226,10 +247,24 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
   for (int j = 0; j < kMelW2; ++j) mw2[j] = melw[64 * kMelW1 + lane * kMelW2 + j];
   const int ws1 = melws[lane], ws2 = melws[64 + lane];
   float ra[20], rb[20];
-  load_pair((int64_t)blockIdx.x * kF2Waves + wv, ra, rb);
+  int ta_cur = lt;   // frame index of the current pass's first row in its utterance
+  load_pair(p_beg < p_end, ra, rb);
   const bool lact = g < kF2Pairs;
-  for (int64_t ps = (int64_t)blockIdx.x * kF2Waves + wv; ps < passes; ps += pstep) {
-    const int ta_cur = ta_next;   // frame index of this pass's first row in its utterance
+  // STATS: the lane's running sums for the current utterance ({x, y}: its two
+  // filters), and the slot of the next one to flush
+  f2 s_run = {0.0f, 0.0f}, q_run = {0.0f, 0.0f};
+  int seg = 0;
+  auto flush = [&]() {   // (wave-uniform) reduce the running sums over the wave into the next slot
+    float t0 = sum_rows4(row16_sum(s_run.x + s_run.y));
+    float t1 = sum_rows4(row16_sum(q_run.x + q_run.y));
+    if (lane == 0) part[wid * MS + seg] = make_float2(t0, t1);
+    ++seg;
+    s_run = f2{0.0f, 0.0f};
+    q_run = f2{0.0f, 0.0f};
+  };
+  for (int64_t ps = p_beg; ps < p_end; ++ps) {
+    const int ta_pass = ta_cur;
+    ta_cur = lt;   // (the next pass's, before load_pair advances it)
     // stage 1: lane (g, n2 = q): DFT-20 over n1 of z[20 n1 + n2] = w (x_a + i x_b)
     f2 v[20];
     {
@@ -247,7 +282,7 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
       }
       asm volatile("" ::: "memory");   // ahead of the next pass's loads
     }
-    load_pair(ps + pstep, ra, rb);
+    load_pair(ps + 1 < p_end, ra, rb);
     dft20(v);
     // A rows: lane (g, q) writes A[g][q][0..19]; pitch 25 float2 = 50 dwords:
     // 50 i mod 64 over 32 lanes is 2 x (25 i mod 32), all distinct
@@ -385,44 +420,31 @@ __global__ __launch_bounds__(kF2Waves * 64, 1) void ctc_logmel_fft2_kernel(const
       }
       if constexpr (STATS) {
         // rows r0 .. r0 + nr - 1; those from bnd on belong to the next utterance
-        const int bnd = T - ta_cur;
+        const int bnd = T - ta_pass;
         const float m2 = half0 ? 1.0f : 0.0f;   // the second filter set counts once per mel (even lanes 0-30)
         const float kLogFloor = wk_logf(1e-8f);   // bit-identical to a silent bin's value
-        // per frame P = {x - K, (y - K) m2} for the lane's two filters; sums {Sx, Sy}, {Qx, Qy}
-        f2 s0 = {0.0f, 0.0f}, q0 = {0.0f, 0.0f}, s1 = {0.0f, 0.0f}, q1 = {0.0f, 0.0f};
+        // per frame P = {x - K, (y - K) m2} for the lane's two filters
         const f2 pm = {1.0f, m2}, pk = {-kLogFloor, -kLogFloor * m2};
+        if (ta_pass == 0 && ps != p_beg) flush();   // the previous pass ended an utterance
         if (bnd >= 6 && nr == 6) {   // the common pass: one utterance, all rows live
 #pragma unroll
           for (int f = 0; f < 6; ++f) {
             const f2 P = fma2(f2{la[f], lc[f]}, pm, pk);
-            s0 = s0 + P;
-            q0 = fma2(P, P, q0);
+            s_run = s_run + P;
+            q_run = fma2(P, P, q_run);
           }
         } else {
 #pragma unroll
           for (int f = 0; f < 6; ++f) {
+            if (f == bnd && f < nr) flush();   // (wave-uniform) the utterance ends inside this pass
             const f2 P = fma2(f2{la[f], lc[f]}, pm, pk);
             if (f < nr) {   // wave-uniform
-              if (f < bnd) {
-                s0 = s0 + P;
-                q0 = fma2(P, P, q0);
-              } else {
-                s1 = s1 + P;
-                q1 = fma2(P, P, q1);
-              }
+              s_run = s_run + P;
+              q_run = fma2(P, P, q_run);
             }
           }
         }
-        const f2 sq0 = {s0.x + s0.y, q0.x + q0.y}, sq1 = {s1.x + s1.y, q1.x + q1.y};
-        float t[4] = {sq0.x, sq0.y, sq1.x, sq1.y};
-        const int nred = bnd < nr ? 4 : 2;   // wave-uniform: slot 1 is empty unless the pass straddles
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (i < nred) t[i] = sum_rows4(row16_sum(t[i]));
-        const __amdgpu_buffer_rsrc_t prs = make_rsrc(part + ps, 16u);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
-                                                                  make_float4(t[0], t[1], t[2], t[3])),
-                                               prs, lane == 0 ? 0 : 0x40000000, 0, 0);
+        if (ps + 1 == p_end) flush();   // the range's last utterance
       }
     }
     wave_lds_sync();
@@ -517,28 +539,31 @@ __global__ __launch_bounds__(1024) void ctc_zscore_kernel(float* __restrict__ fe
 }
 
 // The z-score's statistics for wk_ctc_transcribe: one wave per utterance
-// folds the log-mel passes' {S, Q} partials (ctc_logmel_fft2_kernel<true>) in
-// double into zs[b] = {mean, 1/std} (unbiased std, ctc.py:101-104), or {0, 1}
-// when std is 0 (no normalisation).  Needs T >= 6: a pass then spans at most
-// two utterances.  The partials are float sums, so Q - S m carries ~1e-6 of
+// folds the log-mel waves' {S, Q} slots for it (ctc_logmel_fft2_kernel<true>:
+// wave w's range of R passes starts in utterance 6 w R / T, its j-th slot is
+// that utterance + j) in double into zs[b] = {mean, 1/std} (unbiased std,
+// ctc.py:101-104), or {0, 1} when std is 0 (no normalisation).  Needs T >= 6:
+// a pass then spans at most two utterances.  The partials are float sums, so
+// Q - S m carries ~1e-6 of
 // Q's size in rounding: a variance at or below 1e-5 of the mean square (a
 // constant utterance, silent or not, lands there) is recomputed exactly from
 // the utterance's raw rows, two passes in double -- a constant utterance then
 // gets std 0 exactly and stays un-normalised, as ctc.py:104's `std() > 0` test
 // leaves it.
-__global__ __launch_bounds__(256) void ctc_zstats_kernel(const float4* __restrict__ part, const float* __restrict__ feats,
-                                                         int64_t batch, int T, float2* __restrict__ zs) {
-  // one wave per utterance: lane i takes passes p0 + i, + 64, ...
+__global__ __launch_bounds__(256) void ctc_zstats_kernel(const float2* __restrict__ part, const float* __restrict__ feats,
+                                                         int64_t batch, int T, int64_t R, int MS,
+                                                         float2* __restrict__ zs) {
+  // one wave per utterance: lane i takes the waves w0 + i, + 64, ... whose ranges hold its rows
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= batch) return;   // (wave-uniform)
-  const int64_t r0 = b * T, p0 = r0 / 6, p1 = (r0 + T - 1) / 6;
+  const int64_t r0 = b * T, w0 = r0 / 6 / R, w1 = (r0 + T - 1) / 6 / R;
   double S = 0.0, Q = 0.0;
-  for (int64_t p = p0 + lane; p <= p1; p += 64) {
-    const float4 v = part[p];
-    const bool first = 6 * p >= r0;   // the pass starts in this utterance (slot 0), else it is the pass's slot 1
-    S += first ? v.x : v.z;
-    Q += first ? v.y : v.w;
+  for (int64_t w = w0 + lane; w <= w1; w += 64) {
+    const int64_t first = w * R * 6 / T;   // the utterance of the range's first row
+    const float2 v = part[w * MS + (b - first)];
+    S += v.x;
+    Q += v.y;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1965,9 +1990,9 @@ struct wk_ctc {
   int* best;
   int* best2;           // fp16 mode: the runner-up column of near-tie rows (else -1), for ctc_rescore_kernel
   float* tr_feats;      // wk_ctc_transcribe: [rows][80] features (raw in fp16 mode), pass partials, per-utterance z-score
-  float4* tr_part;
+  float2* tr_part;       // [tr_slots] per-wave log-mel statistics (ctc_logmel_fft2_kernel<true>)
   float2* tr_zs;
-  size_t tr_rows, tr_batch;
+  size_t tr_rows, tr_batch, tr_slots;
   int64_t last_batch;   // geometry of the last wk_ctc_forward (wk_ctc_frame_argmax)
   int32_t last_T;
   // stage timing (wk_ctc_profile): events recorded around each stage on the
@@ -2486,10 +2511,31 @@ wk_status wk_ctc_destroy(wk_ctc* c) {
 }
 
 namespace {
+// The log-mel kernel's launch: at most one 12-wave workgroup per CU, each wave
+// a contiguous range of R passes; MS statistics slots per wave (the most
+// utterances 6 R rows can touch), slots = waves x MS.
+struct LogmelLayout {
+  unsigned grid;
+  int64_t R;
+  int MS;
+  int64_t slots;
+};
+LogmelLayout logmel_layout(const wk_ctc* c, int64_t rows, int T) {
+  LogmelLayout L;
+  const int64_t passes = (rows + 2 * kF2Pairs - 1) / (2 * kF2Pairs);
+  const int64_t blocks = (passes + kF2Waves - 1) / kF2Waves;
+  L.grid = (unsigned)(blocks < c->n_cu ? blocks : c->n_cu);
+  const int64_t nw = (int64_t)L.grid * kF2Waves;
+  L.R = (passes + nw - 1) / nw;
+  L.MS = (int)((2 * kF2Pairs * L.R - 1) / T + 2);
+  L.slots = nw * L.MS;
+  return L;
+}
+
 // wk_ctc_features; with `part` (wk_ctc_transcribe, T >= 6) the features stay
 // raw and the z-score's statistics go to zs instead of being applied in place.
 wk_status ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n_valid, int32_t n_samples,
-                       int64_t stride, float* d_feats, void* stream, float4* part, float2* zs) {
+                       int64_t stride, float* d_feats, void* stream, float2* part, float2* zs) {
   if (!c || batch < 0 || (batch > 0 && (!d_audio || !d_feats)) || n_samples < kNfft / 2 + 1 || n_valid < 0 ||
       (batch > 1 && stride < (n_valid < n_samples ? n_valid : n_samples)))
     return invalid("wk_ctc_features: bad arguments (n_samples must exceed 200 for the reflect pad)");
@@ -2504,23 +2550,24 @@ wk_status ctc_features(wk_ctc* c, const float* d_audio, int64_t batch, int32_t n
     // n_valid == 0: every sample is padding; the kernel's (masked) loads then
     // read a device table instead of a possibly empty audio buffer
     const float* au = nv > 0 ? d_audio : c->fft_win;
+    const LogmelLayout lay = logmel_layout(c, rows, T);
+    if (part && (size_t)lay.slots > c->tr_slots) return invalid("wk_ctc_transcribe: statistics workspace too small");
     wk_status s = timed(c, WK_CTC_STAGE_LOGMEL, st, [&]() -> wk_status {
-      const int64_t passes2 = (rows + 2 * kF2Pairs - 1) / (2 * kF2Pairs);
-      const int64_t blocks2 = (passes2 + kF2Waves - 1) / kF2Waves;
-      const dim3 lg2((unsigned)(blocks2 < c->n_cu ? blocks2 : c->n_cu));
+      const dim3 lg2(lay.grid);
       if (part)
         hipLaunchKernelGGL(ctc_logmel_fft2_kernel<true>, lg2, dim3(kF2Waves * 64), 0, st, au, nv > 0 ? stride : (int64_t)0,
-                           nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->melw, c->melws, d_feats, part);
+                           nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->melw, c->melws, d_feats, lay.R, lay.MS, part);
       else
         hipLaunchKernelGGL(ctc_logmel_fft2_kernel<false>, lg2, dim3(kF2Waves * 64), 0, st, au, nv > 0 ? stride : (int64_t)0,
-                           nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->melw, c->melws, d_feats, (float4*)nullptr);
+                           nv, n_samples, T, rows, c->fft_win, c->fft_tw, c->melw, c->melws, d_feats, lay.R, lay.MS,
+                           (float2*)nullptr);
       return WK_OK;
     });
     if (s == WK_OK)
       s = timed(c, WK_CTC_STAGE_ZSCORE, st, [&]() -> wk_status {
         if (part)
           hipLaunchKernelGGL(ctc_zstats_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, part, d_feats, batch, T,
-                             zs);
+                             lay.R, lay.MS, zs);
         else
           hipLaunchKernelGGL(ctc_zscore_kernel, dim3((unsigned)batch), dim3(1024), 0, st, d_feats, (int64_t)T * kMels);
         return WK_OK;
@@ -2569,6 +2616,7 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
     }
     c->last_batch = batch;
     c->last_T = T;
+    // two 4-wave workgroups per CU: 3 or more measured slower (0.187 -> 0.21-0.22 ms, profiles/r05g_ctc_ab.txt)
     const int enc_grid = (int)((rows + 63) / 64 < 2 * c->n_cu ? (rows + 63) / 64 : 2 * c->n_cu);
     wk_status s = timed(c, WK_CTC_STAGE_ENCODER, st, [&]() -> wk_status {
       if (f16 && zs)
@@ -2727,8 +2775,8 @@ wk_status wk_ctc_transcribe(wk_ctc* c, const float* d_audio, int64_t batch, int3
   return on_device(c->cfg.device, [&]() -> wk_status {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
-    const int64_t passes = (rows + 5) / 6;
-    if ((size_t)rows > c->tr_rows || (size_t)batch > c->tr_batch) {   // grows on first use, then reused
+    const int64_t slots = logmel_layout(c, rows, T).slots;
+    if ((size_t)rows > c->tr_rows || (size_t)batch > c->tr_batch || (size_t)slots > c->tr_slots) {   // grows, then reused
       if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
       (void)hipFree(c->tr_feats);
       (void)hipFree(c->tr_part);
@@ -2736,13 +2784,14 @@ wk_status wk_ctc_transcribe(wk_ctc* c, const float* d_audio, int64_t batch, int3
       c->tr_feats = nullptr;
       c->tr_part = nullptr;
       c->tr_zs = nullptr;
-      c->tr_rows = c->tr_batch = 0;
+      c->tr_rows = c->tr_batch = c->tr_slots = 0;
       if ((e = hipMalloc(&c->tr_feats, sizeof(float) * rows * kMels)) != hipSuccess ||
-          (e = hipMalloc(&c->tr_part, sizeof(float4) * passes)) != hipSuccess ||
+          (e = hipMalloc(&c->tr_part, sizeof(float2) * slots)) != hipSuccess ||
           (e = hipMalloc(&c->tr_zs, sizeof(float2) * batch)) != hipSuccess)
         return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_ctc_transcribe workspace");
       c->tr_rows = (size_t)rows;
       c->tr_batch = (size_t)batch;
+      c->tr_slots = (size_t)slots;
     }
     wk_status s = ctc_features(c, d_audio, batch, n_valid, n_samples, stride, c->tr_feats, stream,
                                fused ? c->tr_part : nullptr, fused ? c->tr_zs : nullptr);

@@ -195,17 +195,30 @@ def _edit_distance(a, b):
 # mix: "out32" = the fp16 path with an fp32 output layer, "out16" = the fp32
 # path with the fp16 output kernel (WAKEWORD_CTC_MIX), "norescore" = the
 # re-scoring off (WAKEWORD_CTC_RESCORE=0): the attribution table of DESIGN 5.3.
+#
+# The counts are chaotic at the level of a few sequences: every flip is a
+# near-tie, so a perturbation far below the fp16 noise moves them.  Round 5
+# measured them under two summation orders of the z-score statistics (per-pass
+# partials, profiles/r05c_ctc_decisions.txt; per-wave running sums,
+# profiles/r05g_ctc_decisions.txt), both exact to ~1e-7 relative: fp16 x4 went
+# 56 -> 52 exact sequences while its re-scoring-off variant went 48 -> 50.  The
+# sequence bounds are the lower of the two minus one or two sequences; the
+# hard parity assertion is on the margins: a decision may differ from the
+# oracle's only where the oracle's own top-2 log-prob margin is below
+# CTC_FLIP_MARGIN (fp16: measured at most 8.0e-4; fp32: 9.5e-7, an fp32
+# rounding-level tie decided by summation order).
 CTC_DECISION_BOUNDS = {
-    # product paths: measured (round 5, profiles/r05c_ctc_decisions.txt) minus one to three sequences of slack
-    ("fp16", 4.0, ""): (0.84, 0.20, 0.9990),           # measured 56/64, 0.141, 0.99922
-    ("fp16", 1.0, ""): (0.72, 0.45, 0.9985),           # measured 49/64, 0.375, 0.99886
-    ("fp32", 4.0, ""): (0.96, 0.05, 0.9999),           # measured 63/64, 0.016, 0.99995 (the flip: oracle margin 9.5e-7)
+    # product paths
+    ("fp16", 4.0, ""): (0.78, 0.32, 0.9988),           # measured 56 / 52 of 64, 0.141 / 0.250, 0.99922 / 0.99907
+    ("fp16", 1.0, ""): (0.66, 0.52, 0.9982),           # measured 49 / 44, 0.375 / 0.438, 0.99886 / 0.99849
+    ("fp32", 4.0, ""): (0.96, 0.05, 0.9999),           # measured 63 / 63, 0.016, 0.99995
     # attribution: re-scoring off, one stage's precision swapped
-    ("fp16", 4.0, "norescore"): (0.70, 0.40, 0.9985),  # measured 48/64, 0.328, 0.99875
-    ("fp16", 1.0, "norescore"): (0.70, 0.50, 0.9985),  # measured 49/64, 0.406, 0.99881
-    ("fp16", 4.0, "out32"): (0.84, 0.20, 0.9990),      # measured 56/64, 0.141, 0.99922
-    ("fp32", 4.0, "out16+norescore"): (0.75, 0.35, 0.9985),   # measured 51/64, 0.297, 0.99891
+    ("fp16", 4.0, "norescore"): (0.70, 0.40, 0.9985),  # measured 48 / 50, 0.328 / 0.328, 0.99875 / 0.99881
+    ("fp16", 1.0, "norescore"): (0.66, 0.52, 0.9982),  # measured 49 / 45, 0.406 / 0.438, 0.99881 / 0.99855
+    ("fp16", 4.0, "out32"): (0.78, 0.32, 0.9988),      # measured 56 / 52, 0.141 / 0.250, 0.99922 / 0.99907
+    ("fp32", 4.0, "out16+norescore"): (0.75, 0.35, 0.9985),   # measured 51 / 51, 0.297, 0.99891
 }
+CTC_FLIP_MARGIN = {"fp16": 2e-3, "fp32": 1e-5}
 
 
 @pytest.mark.parametrize("precision,out_scale,mix", list(CTC_DECISION_BOUNDS))
@@ -257,3 +270,6 @@ def test_config5_decision_parity(precision, out_scale, mix, monkeypatch):
           f"(oracle mean length {ntok / len(idx):.1f}), frame-argmax agreement {frame_agree:.5f}")
     lo_match, hi_dist, lo_frame = CTC_DECISION_BOUNDS[(precision, out_scale, mix)]
     assert match >= lo_match and mean_dist <= hi_dist and frame_agree >= lo_frame, (match, mean_dist, frame_agree)
+    # confident frames decide exactly as the oracle does (the fp16 margin wherever an fp16 stage is in the path)
+    bound = CTC_FLIP_MARGIN["fp16" if precision == "fp16" or "out16" in mix else "fp32"]
+    assert margins.numel() == 0 or float(margins.max()) <= bound, float(margins.max())
