@@ -1554,16 +1554,19 @@ __device__ __forceinline__ int out_chunk(int n, int c) { return c ^ (n & 15); }
 constexpr int out_rf(bool logits) { return logits ? 2 : kOutRF; }
 constexpr int out_rows(bool logits) { return 16 * out_rf(logits) * kOutWaves; }
 // KEYED (V <= 4096, so 4 NT <= 256): the running maximum carries its column
-// in the value's low 8 mantissa bits, so the epilogue is two VALU per value
-// and one v_max3_f32 per two values instead of compare + two selects per
-// value.  The tag is 255 - (4 tile + cf) for a positive value and 4 tile + cf
-// for a negative one (v_perm_b32 spreads the sign bit over the low byte, the
-// XOR with the tag finishes it): an earlier column then always makes the
-// larger tagged value, whichever the sign, so equal logits keep the first
-// index, as torch.argmax does (ctc.py:454).  The column is 16 (4 tile + cf) + li.
-// A tagged value moves by < 2^-15 of itself: the first maximum is exact except
-// between logits that agree to within that (fp16 operands already put ~1e-3 of
-// noise on every logit); the tokens stay a function of the row alone.
+// in the value's low 8 mantissa bits, so the epilogue is one VALU per value
+// (v_and_or_b32) and one v_max3_f32 per two values instead of compare + two
+// selects per value.  The tag is 255 - (4 tile + cf): among values whose
+// upper 24 bits agree, an earlier column makes the larger tagged value when
+// they are positive, so equal logits keep the first index, as torch.argmax
+// does (ctc.py:454).  Between negative values the tag orders the other way
+// (round 4 spread the sign into the tag with a v_perm_b32 first: two VALU per
+// value); such a tie is within 2^-15 of the row's maximum, which makes the
+// row a near-tie that ctc_rescore_kernel decides again in fp32 with the
+// first-index rule.  The column is 16 (4 tile + cf) + li.  A tagged value
+// moves by < 2^-15 of itself: the first maximum is exact except between
+// logits that agree to within that (fp16 operands already put ~1e-3 of noise
+// on every logit); the tokens stay a function of the row alone.
 // m = max(m, k0, k1) on the tagged values (fmaxf would first canonicalise
 // each of them: they come from integer ops).  The tags are applied in C++, so
 // the compiler still places the wait states for reading MFMA results.
@@ -1572,21 +1575,16 @@ __device__ __forceinline__ float out_max3(float m, float k0, float k1) {
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(k0), "v"(k1));
   return r;
 }
-// sel = 0x03020109: bytes 3..1 of x, byte 0 = x's sign bit replicated (v_perm_b32 selector 9)
-__device__ __forceinline__ float out_tag(float x, unsigned sel, unsigned tag) {
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  return __builtin_bit_cast(float, __builtin_amdgcn_perm(u, u, sel) ^ tag);
+// mask = 0xffffff00 (in a VGPR: VOP3 takes no literal), tag in an SGPR
+__device__ __forceinline__ float out_tag(float x, unsigned mask, unsigned tag) {
+  return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, x) & mask) | tag);
 }
 // Runner-up tracking (KEYED): the second largest of {m, k0, k1} is their
-// median; the row's running second maximum is max(m2, med3(m, k0, k1)).
+// median; the row's running second maximum is max(m2, med3(m, k0, k1)), and
+// over four values max3(m2, med3(m, k0, k1), med3(max3(m, k0, k1), k2, k3)).
 __device__ __forceinline__ float out_med3(float a, float b, float c) {
   float r;
   asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-__device__ __forceinline__ float out_max(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
 // Near-tie re-scoring (decision parity): a row whose top-2 tagged
@@ -1598,10 +1596,7 @@ __device__ __forceinline__ bool out_near_tie(float m1, float m2) {
 }
 
 // The column block (4 tile + cf) of a tagged value.
-__device__ __forceinline__ int out_untag(float m) {
-  const unsigned u = __builtin_bit_cast(unsigned, m);
-  return (int)(((u & 255u) ^ ((u >> 31) ? 0u : 255u)));
-}
+__device__ __forceinline__ int out_untag(float m) { return (int)(255u - (__builtin_bit_cast(unsigned, m) & 255u)); }
 template <bool LOGITS, bool KEYED>
 __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const __half* __restrict__ y,
                                                                           const __half* __restrict__ w,
@@ -1684,8 +1679,8 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
   __syncthreads();
   float mx[kOutRF][4], mx2[kOutRF][4];   // (mx2: KEYED runner-up)
   int ix[kOutRF][4];
-  unsigned ksel;   // (KEYED) the v_perm_b32 selector of out_tag, in a VGPR (VOP3 takes no literal)
-  asm("v_mov_b32 %0, 0x03020109" : "=v"(ksel));
+  unsigned kmask;   // (KEYED) out_tag's mask, in a VGPR (VOP3 takes no literal)
+  asm("v_mov_b32 %0, 0xffffff00" : "=v"(kmask));
 #pragma unroll
   for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
@@ -1720,19 +1715,24 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
               if ((decltype(full)::value || v < V) && r < rows) logits[r * V + v] = __float2half(acc[rf][cf][i]);
             }
         }
-        if (cf & 1) {   // columns cf - 1 and cf: two tagged values per v_max3_f32
+        static_assert(kOutCF == 4, "the epilogue folds the tile's four column blocks at once");
+        if (cf == kOutCF - 1) {   // all four column blocks: four tagged values per two v_max3_f32
 #pragma unroll
           for (int rf = 0; rf < kOutRF; ++rf)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              float x0 = acc[rf][cf - 1][i], x1 = acc[rf][cf][i];
-              if (!decltype(full)::value) {   // (-FLT_MAX: tagged -inf would be a NaN)
-                x0 = v - 16 < V ? x0 : -FLT_MAX;
-                x1 = v < V ? x1 : -FLT_MAX;
+              float x[4];
+#pragma unroll
+              for (int c = 0; c < 4; ++c) {   // (-FLT_MAX past V: tagged -inf would be a NaN)
+                x[c] = acc[rf][c][i];
+                if (!decltype(full)::value) x[c] = tile * kOutBN + 16 * c + li < V ? x[c] : -FLT_MAX;
               }
-              const float t0 = out_tag(x0, ksel, tag + 1), t1 = out_tag(x1, ksel, tag), m = mx[rf][i];
-              mx2[rf][i] = out_max(mx2[rf][i], out_med3(m, t0, t1));
-              mx[rf][i] = out_max3(m, t0, t1);
+              const float t0 = out_tag(x[0], kmask, tag + 3), t1 = out_tag(x[1], kmask, tag + 2);
+              const float t2 = out_tag(x[2], kmask, tag + 1), t3 = out_tag(x[3], kmask, tag);
+              const float m = mx[rf][i], a = out_med3(m, t0, t1), m1 = out_max3(m, t0, t1);
+              const float b = out_med3(m1, t2, t3);
+              mx[rf][i] = out_max3(m1, t2, t3);
+              mx2[rf][i] = out_max3(mx2[rf][i], a, b);
             }
         }
       } else if (decltype(full)::value || v < V) {
