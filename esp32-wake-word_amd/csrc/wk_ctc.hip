@@ -1826,6 +1826,191 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
     }
 }
 
+// Decode-only form of the kernel above (KEYED, no logits: wk_ctc_transcribe's
+// path), with the epilogue moved in among the MFMAs.  Here a tile's four
+// column blocks are computed in two halves (blocks 0-1, then
+// 2-3), and each half's 48 MFMAs carry the epilogue of the OTHER half's
+// finished accumulators (blocks 2-3 of the previous tile, then blocks 0-1 of
+// this one), placed between them by sched_group_barrier: the fold's VALU goes
+// into the cycles a v_mfma_f32_16x16x32_f16 leaves (8 of its 16), with no
+// second set of accumulators.  Both waves of a SIMD run the same schedule (no
+// skew).  Columns past V get bias -1e30 and read W rows of 0, so no tile needs
+// a bound check; the first tile's dummy fold reads accumulators preset to
+// -1e30.  Tokens are bit-identical to ctc_out_argmax16_kernel<false, true>
+// (same accumulation order per logit, same tags and folds per value).
+__device__ __forceinline__ float out_max(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__global__ __launch_bounds__(kOutWaves * 64) void ctc_out_decode16_kernel(const __half* __restrict__ y,
+                                                                          const __half* __restrict__ w,
+                                                                          const float* __restrict__ bias, int64_t rows,
+                                                                          int V, int* __restrict__ best,
+                                                                          int* __restrict__ best2) {
+  constexpr int RF = kOutRF, kRows = 16 * RF * kOutWaves;
+  // Two separate W buffers (and bias buffers), selected at compile time: the
+  // compiler then knows the LDS-DMA into one cannot alias the B-fragment reads
+  // of the other, so a period can start the next tile's DMA and still read its
+  // own tile without waiting for it (with one array it waits at the first read).
+  __shared__ __attribute__((aligned(1024))) _Float16 bt0[kOutBN * kOutPitch];
+  __shared__ __attribute__((aligned(1024))) _Float16 bt1[kOutBN * kOutPitch];
+  __shared__ f32x4 bsh0[kOutBN], bsh1[kOutBN];   // the tile's bias x4 (an MFMA C operand)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wvu = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lg = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * kRows + 16 * RF * wvu;
+  h8 a[RF][8];   // A fragments: rows row0 + 16 rf + li, k = 32 st + 8 lg .. +7
+#pragma unroll
+  for (int rf = 0; rf < RF; ++rf) {
+    const int64_t r = row0 + 16 * rf + li;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      if (r < rows) {   // non-temporal, as above
+        const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(y + r * kOutK + 32 * st + 8 * lg));
+        v = make_uint4(t[0], t[1], t[2], t[3]);
+      }
+      a[rf][st] = __builtin_bit_cast(h8, v);
+    }
+  }
+  const int NT = (V + kOutBN - 1) / kOutBN;
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(w, (uint32_t)V * kOutK * 2);
+  const __amdgpu_buffer_rsrc_t brs = make_rsrc(bias, (uint32_t)V * 4);
+  // W tiles by LDS-DMA (as above), 4 pieces per wave, all 8 waves
+  constexpr int kDmaPer = kOutBN * kOutK * 2 / 1024 / kOutWaves;
+  int dma_off[kDmaPer];
+#pragma unroll
+  for (int i = 0; i < kDmaPer; ++i) {
+    const int q = wvu * kDmaPer + i, rr = 2 * q + (lane >> 5), c = (lane & 31) ^ (rr & 15);
+    dma_off[i] = rr * (kOutK * 2) + 16 * c;
+  }
+  auto dma_w = [&](_Float16* dst, int nt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < kDmaPer; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)&dst[(wvu * kDmaPer + i) * 512],
+                                               16, dma_off[i], nt * (kOutBN * kOutK * 2), 0, 0);
+  };
+  float pb = 0.0f;
+  auto fetch = [&](int nt) {   // wave 0: the tile's bias (used at stash: no wait here)
+    if (wvu == 0) pb = buf_load(brs, 4 * (nt * kOutBN + lane), 0);
+  };
+  auto stash = [&](f32x4* dst, int nt) {   // -1e30 past V
+    const float v = nt * kOutBN + lane < V ? pb : -1e30f;
+    if (wvu == 0) dst[lane] = f32x4{v, v, v, v};
+  };
+  fetch(0);
+  stash(bsh0, 0);
+  dma_w(bt0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float mx[RF][4], mx2[RF][4];
+  f32x4 acc[RF][kOutCF];
+#pragma unroll
+  for (int rf = 0; rf < RF; ++rf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { mx[rf][i] = -INFINITY; mx2[rf][i] = -INFINITY; }
+#pragma unroll
+    for (int cf = 2; cf < kOutCF; ++cf) acc[rf][cf] = f32x4{-1e30f, -1e30f, -1e30f, -1e30f};   // the first dummy fold
+  }
+  unsigned kmask;   // out_tag's mask, in a VGPR (VOP3 takes no literal)
+  asm("v_mov_b32 %0, 0xffffff00" : "=v"(kmask));
+  // One half: blocks 2h and 2h + 1 of the tile in (b, bs) (16 steps of one B
+  // fragment x RF MFMAs; fragments read two steps ahead), with the fold of
+  // blocks 2eh, 2eh + 1 of tile etile (12 items of 5 VALU) spread one item per
+  // step; a sched_barrier after each step keeps that order.
+  auto half = [&](const _Float16* b, const f32x4* bs, int h, int etile, int eh) __attribute__((always_inline)) {
+    auto frag = [&](int s) -> h8 {
+      const int cf = 2 * h + (s >> 3), st = s & 7;
+      return *reinterpret_cast<const h8*>(b + (16 * cf + li) * kOutPitch + 8 * out_chunk(li, 4 * st + lg));
+    };
+    const unsigned tag = 255u - (unsigned)(kOutCF * etile + 2 * eh);   // block 2eh; block 2eh + 1: tag - 1
+    constexpr int PD = 4;   // fragment prefetch distance in steps (2: +1.5 % time; profiles/r05p_dec16_variants_ab.txt)
+    f32x4 c0 = bs[16 * (2 * h) + li];
+    h8 ring[PD + 1];
+#pragma unroll
+    for (int q = 0; q < PD; ++q) ring[q] = frag(q);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int cf = 2 * h + (s >> 3), st = s & 7;
+      if (s + PD < 16) ring[(s + PD) % (PD + 1)] = frag(s + PD);
+      if (s == 8) c0 = bs[16 * cf + li];
+      const h8 bf = ring[s % (PD + 1)];
+#pragma unroll
+      for (int rf = 0; rf < RF; ++rf)
+        acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rf][st], bf, st == 0 ? c0 : acc[rf][cf], 0, 0, 0);
+      if (s < RF * 4) {   // fold item s: row block rf, row i
+        const int rf = s >> 2, i = s & 3;
+        const float t0 = out_tag(acc[rf][2 * eh][i], kmask, tag), t1 = out_tag(acc[rf][2 * eh + 1][i], kmask, tag - 1);
+        const float m = mx[rf][i];
+        mx2[rf][i] = out_max(mx2[rf][i], out_med3(m, t0, t1));
+        mx[rf][i] = out_max3(m, t0, t1);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // (without: the compiler clusters the fold, +1.5-3 % time)
+    }
+  };
+  // One period: tile nt from (b, bs); the next tile's W and bias go into (nb, nbs)
+  // at its start (the other buffers were last read in the previous period).
+  auto period = [&](const _Float16* b, const f32x4* bs, _Float16* nb, f32x4* nbs, int nt) __attribute__((always_inline)) {
+    const bool more = nt + 1 < NT;
+    if (more) {
+      fetch(nt + 1);
+      dma_w(nb, nt + 1);
+    }
+    half(b, bs, 0, nt > 0 ? nt - 1 : 0, 1);   // blocks 0-1 || fold of the previous tile's blocks 2-3
+    half(b, bs, 1, nt, 0);                    // blocks 2-3 || fold of this tile's blocks 0-1
+    if (more) stash(nbs, nt + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // LDS-DMA done (the barrier's own wait omits it)
+    __syncthreads();
+  };
+  for (int nt = 0; nt < NT; nt += 2) {
+    period(bt0, bsh0, bt1, bsh1, nt);
+    if (nt + 1 < NT) period(bt1, bsh1, bt0, bsh0, nt + 1);
+  }
+  {   // the last tile's blocks 2-3
+    const unsigned tag = 255u - (unsigned)(kOutCF * (NT - 1) + 2);
+#pragma unroll
+    for (int rf = 0; rf < RF; ++rf)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float t0 = out_tag(acc[rf][2][i], kmask, tag), t1 = out_tag(acc[rf][3][i], kmask, tag - 1);
+        const float m = mx[rf][i];
+        mx2[rf][i] = out_max(mx2[rf][i], out_med3(m, t0, t1));
+        mx[rf][i] = out_max3(m, t0, t1);
+      }
+  }
+  // first maximum across the 16 column lanes of each row (as above)
+#pragma unroll
+  for (int rf = 0; rf < RF; ++rf)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float m = mx[rf][i], m2 = mx2[rf][i];
+      int k = 16 * out_untag(m) + li, k2 = 16 * out_untag(m2) + li;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float om = __shfl_xor(m, o, 64), om2 = __shfl_xor(m2, o, 64);
+        const int ok = __shfl_xor(k, o, 64), ok2 = __shfl_xor(k2, o, 64);
+        const bool other_wins = om > m || (om == m && ok < k);
+        const float lm = other_wins ? m : om;
+        const int lk = other_wins ? k : ok;
+        const bool r_other = om2 > m2 || (om2 == m2 && ok2 < k2);
+        const float rm = r_other ? om2 : m2;
+        const int rk = r_other ? ok2 : k2;
+        const bool use_loser = lm > rm || (lm == rm && lk < rk);
+        m2 = use_loser ? lm : rm;
+        k2 = use_loser ? lk : rk;
+        if (other_wins) { m = om; k = ok; }
+      }
+      const int64_t r = row0 + 16 * rf + 4 * lg + i;
+      if (li == 0 && r < rows) {
+        best[r] = k;
+        best2[r] = m2 > -INFINITY && out_near_tie(m, m2) ? k2 : -1;
+      }
+    }
+}
+
 // Near-tie re-scoring after ctc_out_argmax16_kernel (fp16 mode, V <= 4096):
 // a row whose top-2 logits came within out_near_tie of each other is decided
 // between those two columns again with fp32 weights (y is the fp16 GRU output,
@@ -2705,9 +2890,12 @@ wk_status ctc_forward(wk_ctc* c, const float* d_feats, int64_t batch, int32_t T,
           hipLaunchKernelGGL(ctc_argmax_kernel<__half>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st,
                              c->logits16, c->zero_b, rows, V, d_log_probs, (int*)nullptr, (int)batch, T);   // bias already in
         } else {
-          hipLaunchKernelGGL((keyed ? ctc_out_argmax16_kernel<false, true> : ctc_out_argmax16_kernel<false, false>), og,
-                             dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b, rows, V, (__half*)nullptr,
-                             c->best, c->best2);
+          if (keyed)   // the decode-only kernel, the fold among the MFMAs
+            hipLaunchKernelGGL(ctc_out_decode16_kernel, og, dim3(kOutWaves * 64), 0, st, c->y1h, c->out_w16, c->out_b,
+                               rows, V, c->best, c->best2);
+          else
+            hipLaunchKernelGGL((ctc_out_argmax16_kernel<false, false>), og, dim3(kOutWaves * 64), 0, st, c->y1h,
+                               c->out_w16, c->out_b, rows, V, (__half*)nullptr, c->best, c->best2);
         }
         if (keyed && c->rescore)   // near-tie rows decided again in fp32 (tokens independent of log-probs: both variants)
           hipLaunchKernelGGL(ctc_rescore_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, c->y1h,

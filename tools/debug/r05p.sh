@@ -2,4 +2,4 @@
 set -o pipefail
 O=$PWD/gpurun_out/r05p
 mkdir -p $O
-bash tools/debug/ctc_ab.sh dec16b dec16c dec16d dec16e 2>&1 | tee $O/ab.txt
+bash tools/debug/ctc_ab.sh dec16b dec16c dec16d dec16e dec16f 2>&1 | tee $O/ab.txt
