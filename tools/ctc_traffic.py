@@ -13,7 +13,8 @@ MAP = [("ctc_logmel_fft", ["logmel"]), ("ctc_zscore_kernel", ["zscore"]), ("ctc_
        ("ctc_proj16_kernel", ["proj0", "proj1"]), ("Cijk", ["proj0", "proj1"]),
        ("ctc_gru16x_kernelILi128", ["gru0"]), ("ctc_gru16x_kernelILi256", ["gru1"]),
        ("ctc_gru16_kernel", ["gru0", "gru1"]), ("ctc_gru_kernel", ["gru0", "gru1"]),
-       ("ctc_out_argmax16_kernel", ["output"]), ("ctc_greedy_kernel", ["decode"])]
+       ("ctc_out_argmax16_kernel", ["output"]), ("ctc_out_decode16_kernel", ["output"]),
+       ("ctc_greedy_kernel", ["decode"])]
 
 
 def main():
