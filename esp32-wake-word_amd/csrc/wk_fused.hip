@@ -810,7 +810,32 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
 #endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
+#ifdef WK_DIAG_SIMD_SPLIT
+  // Diagnostic (K = 32 question): the roles by hardware SIMD --
+  // front-end waves on SIMDs 0-1, CNN waves on SIMDs 2-3 -- instead of by wave
+  // index (which puts two of each role on every SIMD).  HW_ID bits 5:4 are the
+  // SIMD; a per-SIMD LDS counter gives the slot.  A SIMD with more than four
+  // waves leaves the default mapping (and is reported in err bit 8).
+  __shared__ unsigned simd_slot[4];
+  if (tid < 4) simd_slot[tid] = 0;
+  __syncthreads();
+  int wave;
+  {
+    const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // hwreg(HW_REG_HW_ID, 0, 32)
+    const int simd = (int)((hw >> 4) & 3u);
+    unsigned slot = 0;
+    if (lane == 0) slot = atomicAdd(&simd_slot[simd], 1u);
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    wave = (simd >> 1) * 8 + (simd & 1) * 4 + (int)slot;
+    if (slot > 3u) {
+      wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+      if (lane == 0) atomicOr(err, 256u);
+    }
+    wave = __builtin_amdgcn_readfirstlane(wave);
+  }
+#else
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#endif
   fe_init_tables<true, true>(smem, tid, kFusedBlock);
   for (int i = tid; i < kFusedLds - kGOff; i += kFusedBlock) smem[kGOff + i] = 0.0f;  // ctrl, guards, pads
   __syncthreads();
