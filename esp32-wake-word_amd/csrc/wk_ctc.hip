@@ -1838,11 +1838,6 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 // a bound check; the first tile's dummy fold reads accumulators preset to
 // -1e30.  Tokens are bit-identical to ctc_out_argmax16_kernel<false, true>
 // (same accumulation order per logit, same tags and folds per value).
-__device__ __forceinline__ float out_max(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
 __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_decode16_kernel(const __half* __restrict__ y,
                                                                           const __half* __restrict__ w,
                                                                           const float* __restrict__ bias, int64_t rows,
@@ -1916,6 +1911,11 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_decode16_kernel(const 
   }
   unsigned kmask;   // out_tag's mask, in a VGPR (VOP3 takes no literal)
   asm("v_mov_b32 %0, 0xffffff00" : "=v"(kmask));
+  float carry[RF][4];   // a tile's blocks 0-1 median, folded with its blocks 2-3 (the runner-up, 4 values at once)
+#pragma unroll
+  for (int rf = 0; rf < RF; ++rf)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) carry[rf][i] = -INFINITY;
   // One half: blocks 2h and 2h + 1 of the tile in (b, bs) (16 steps of one B
   // fragment x RF MFMAs; fragments read two steps ahead), with the fold of
   // blocks 2eh, 2eh + 1 of tile etile (12 items of 5 VALU) spread one item per
@@ -1945,7 +1945,11 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_decode16_kernel(const 
         const int rf = s >> 2, i = s & 3;
         const float t0 = out_tag(acc[rf][2 * eh][i], kmask, tag), t1 = out_tag(acc[rf][2 * eh + 1][i], kmask, tag - 1);
         const float m = mx[rf][i];
-        mx2[rf][i] = out_max(mx2[rf][i], out_med3(m, t0, t1));
+        if (eh == 0) {   // one runner-up update per tile: blocks 0-1's median waits for blocks 2-3's (-1 VALU / 4 logits)
+          carry[rf][i] = out_med3(m, t0, t1);
+        } else {
+          mx2[rf][i] = out_max3(mx2[rf][i], carry[rf][i], out_med3(m, t0, t1));
+        }
         mx[rf][i] = out_max3(m, t0, t1);
       }
       __builtin_amdgcn_sched_barrier(0);   // (without: the compiler clusters the fold, +1.5-3 % time)
@@ -1977,7 +1981,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_decode16_kernel(const 
       for (int i = 0; i < 4; ++i) {
         const float t0 = out_tag(acc[rf][2][i], kmask, tag), t1 = out_tag(acc[rf][3][i], kmask, tag - 1);
         const float m = mx[rf][i];
-        mx2[rf][i] = out_max(mx2[rf][i], out_med3(m, t0, t1));
+        mx2[rf][i] = out_max3(mx2[rf][i], carry[rf][i], out_med3(m, t0, t1));
         mx[rf][i] = out_max3(m, t0, t1);
       }
   }
