@@ -1959,7 +1959,7 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_decode16_kernel(const 
   // at its start (the other buffers were last read in the previous period).
   auto period = [&](const _Float16* b, const f32x4* bs, _Float16* nb, f32x4* nbs, int nt) __attribute__((always_inline)) {
     const bool more = nt + 1 < NT;
-    if (more) {
+    if (more) {   // (the pieces spread among the MFMAs, one per 4 steps, or s_setprio 1 for waves 4-7: within +-1 %)
       fetch(nt + 1);
       dma_w(nb, nt + 1);
     }
