@@ -1827,17 +1827,19 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_argmax16_kernel(const 
 }
 
 // Decode-only form of the kernel above (KEYED, no logits: wk_ctc_transcribe's
-// path), with the epilogue moved in among the MFMAs.  Here a tile's four
-// column blocks are computed in two halves (blocks 0-1, then
-// 2-3), and each half's 48 MFMAs carry the epilogue of the OTHER half's
-// finished accumulators (blocks 2-3 of the previous tile, then blocks 0-1 of
-// this one), placed between them by sched_group_barrier: the fold's VALU goes
-// into the cycles a v_mfma_f32_16x16x32_f16 leaves (8 of its 16), with no
-// second set of accumulators.  Both waves of a SIMD run the same schedule (no
-// skew).  Columns past V get bias -1e30 and read W rows of 0, so no tile needs
-// a bound check; the first tile's dummy fold reads accumulators preset to
-// -1e30.  Tokens are bit-identical to ctc_out_argmax16_kernel<false, true>
-// (same accumulation order per logit, same tags and folds per value).
+// path), with the epilogue moved in among the MFMAs.  A tile's four
+// column blocks are computed in two halves (blocks 0-1, then 2-3); each half's
+// 48 MFMAs carry the fold of the OTHER half's finished accumulators (blocks
+// 2-3 of the previous tile, then blocks 0-1 of this one), one item per k-step
+// with a sched_barrier after each, so the fold's VALU goes into the cycles a
+// v_mfma_f32_16x16x32_f16 leaves (8 of its 16) with no second accumulator set.
+// Both waves of a SIMD run the same schedule (no skew).  The next tile's W
+// goes into the other LDS buffer by DMA at the start of the period (separate
+// arrays: the compiler sees they cannot alias, so no read waits for it).
+// Columns past V get bias -1e30 and read W rows of 0, so no tile needs a
+// bound check; the first tile's dummy fold reads accumulators preset to -1e30.
+// Tokens are the same as ctc_out_argmax16_kernel<false, true>'s (same
+// accumulation order per logit, same tags; the folds take exact max/median).
 __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_decode16_kernel(const __half* __restrict__ y,
                                                                           const __half* __restrict__ w,
                                                                           const float* __restrict__ bias, int64_t rows,
