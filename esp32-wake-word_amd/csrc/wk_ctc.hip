@@ -2017,30 +2017,44 @@ __global__ __launch_bounds__(kOutWaves * 64) void ctc_out_decode16_kernel(const 
     }
 }
 
-// Near-tie re-scoring after ctc_out_argmax16_kernel (fp16 mode, V <= 4096):
-// a row whose top-2 logits came within out_near_tie of each other is decided
-// between those two columns again with fp32 weights (y is the fp16 GRU output,
-// widened exactly): bias + sum_k y[k] W[c][k] as an fp32 fmaf chain, the
-// larger wins, an exact tie keeps the smaller column (torch.argmax).  Rows
-// with best2 < 0 keep their fp16 decision.  One thread per row.
+// Near-tie re-scoring after the fp16 output kernels (V <= 4096): a row whose
+// top-2 logits came within out_near_tie of each other is decided between those
+// two columns again with fp32 weights (y is the fp16 GRU output, widened
+// exactly): bias + sum_k y[k] W[c][k] in fp32, the larger wins, an exact tie
+// keeps the smaller column (torch.argmax).  Rows with best2 < 0 keep their fp16
+// decision.  A wave takes 64 consecutive rows, finds the flagged ones with a
+// ballot and re-scores them one at a time with all 64 lanes (4 k per lane, a
+// shuffle-tree sum): the flagged rows are a few percent, and one thread per row
+// walking a 256-long dependent FMA chain had cost ~0.11 ms per batch.
 __global__ __launch_bounds__(256) void ctc_rescore_kernel(const __half* __restrict__ y, const float* __restrict__ w,
                                                           const float* __restrict__ bias, int64_t rows,
                                                           int* __restrict__ best, const int* __restrict__ best2) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= rows) return;
-  const int c2 = best2[r];
-  if (c2 < 0) return;
-  const int c1 = best[r];
-  const __half* yr = y + r * (2 * kH);
-  const float* w1 = w + (int64_t)c1 * (2 * kH);
-  const float* w2 = w + (int64_t)c2 * (2 * kH);
-  float s1 = bias[c1], s2 = bias[c2];
-  for (int k = 0; k < 2 * kH; ++k) {
-    const float yk = __half2float(yr[k]);
-    s1 = __builtin_fmaf(yk, w1[k], s1);
-    s2 = __builtin_fmaf(yk, w2[k], s2);
+  const int lane = threadIdx.x & 63;
+  const int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (base >= rows) return;   // (wave-uniform)
+  const int64_t r = base + lane;
+  const int c2l = r < rows ? best2[r] : -1;
+  uint64_t mask = __ballot(c2l >= 0);
+  while (mask) {   // (wave-uniform)
+    const int j = __builtin_ctzll(mask);
+    mask &= mask - 1;
+    const int64_t rj = base + j;
+    const int c2 = __shfl(c2l, j, 64), c1 = best[rj];
+    const __half2* yr = reinterpret_cast<const __half2*>(y + rj * (2 * kH)) + 2 * lane;
+    const float4 w1 = reinterpret_cast<const float4*>(w + (int64_t)c1 * (2 * kH))[lane];
+    const float4 w2 = reinterpret_cast<const float4*>(w + (int64_t)c2 * (2 * kH))[lane];
+    const float2 ya = __half22float2(yr[0]), yb = __half22float2(yr[1]);
+    float s1 = __builtin_fmaf(ya.x, w1.x, __builtin_fmaf(ya.y, w1.y, __builtin_fmaf(yb.x, w1.z, yb.y * w1.w)));
+    float s2 = __builtin_fmaf(ya.x, w2.x, __builtin_fmaf(ya.y, w2.y, __builtin_fmaf(yb.x, w2.z, yb.y * w2.w)));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    s1 += bias[c1];
+    s2 += bias[c2];
+    if (lane == 0 && (s2 > s1 || (s2 == s1 && c2 < c1))) best[rj] = c2;
   }
-  if (s2 > s1 || (s2 == s1 && c2 < c1)) best[r] = c2;
 }
 
 // Window starts of ctc_logmel_fft2_kernel's straight-line filterbank.  A tap
