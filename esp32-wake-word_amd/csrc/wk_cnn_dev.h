@@ -82,7 +82,12 @@ typedef short s8 __attribute__((ext_vector_type(8)));   // one lane's A or B fra
 #endif
 __device__ __forceinline__ f32x4 mfma_bf16(s8 a, s8 b, f32x4 c) {
 #ifdef WK_MFMA_K32   // diagnostic only (tools/debug/xdl_hazard_scan.py, k32_repeat.py)
+#ifdef WK_K32_F16    // the f16 K = 32 form on the same bit patterns (logits wrong; the features are the probe)
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+#else
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+#endif
 #ifdef WK_K32_PAD   // 16 wait states after every K = 32 MFMA, nothing scheduled across them
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
