@@ -80,25 +80,39 @@ typedef short s8 __attribute__((ext_vector_type(8)));   // one lane's A or B fra
 #if defined(WK_MFMA_K32) && !defined(WK_ALLOW_K32_DIAG)
 #error "WK_MFMA_K32 corrupts the fused kernel's front-end (DESIGN.md 5.1); diagnostic builds add -DWK_ALLOW_K32_DIAG"
 #endif
+#ifndef WK_K32_MASK
+#define WK_K32_MASK 7   // diagnostic K = 32 builds: which conv layers use it (bit 0 conv1, 1 conv2, 2 conv3)
+#endif
+// K32 is true only in diagnostic builds (tools/debug/xdl_hazard_scan.py, k32_repeat.py).
+template <bool K32>
 __device__ __forceinline__ f32x4 mfma_bf16(s8 a, s8 b, f32x4 c) {
-#ifdef WK_MFMA_K32   // diagnostic only (tools/debug/xdl_hazard_scan.py, k32_repeat.py)
+  if constexpr (K32) {
 #ifdef WK_K32_F16    // the f16 K = 32 form on the same bit patterns (logits wrong; the features are the probe)
-  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+    typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 #else
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 #endif
 #ifdef WK_K32_PAD   // 16 wait states after every K = 32 MFMA, nothing scheduled across them
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 #endif
-  return c;
-#endif
+    return c;
+  }
   c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 0, 1, 2, 3),
                                                 __builtin_shufflevector(b, b, 0, 1, 2, 3), c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 4, 5, 6, 7),
                                                    __builtin_shufflevector(b, b, 4, 5, 6, 7), c, 0, 0, 0);
+}
+// the conv layer of a CINP (16: conv1, 32: conv2, 64: conv3) uses the K = 32 form
+template <int CINP>
+constexpr bool k32_layer() {
+#ifdef WK_MFMA_K32
+  return (WK_K32_MASK >> (CINP == 16 ? 0 : CINP == 32 ? 1 : 2)) & 1;
+#else
+  return false;
+#endif
 }
 
 __device__ __forceinline__ uint32_t bf16_bits(float x) {   // round to nearest even
@@ -133,8 +147,8 @@ __device__ __forceinline__ void conv_pair_bf(const uint16_t* __restrict__ img, c
     const int off = kofs<CINP, CIP>(s, g);
     const s8 ba = *reinterpret_cast<const s8*>(img + boff_a + off);
     const s8 bb = *reinterpret_cast<const s8*>(img + boff_b + off);
-    acc_a = mfma_bf16(wf[s], ba, acc_a);
-    acc_b = mfma_bf16(wf[s], bb, acc_b);
+    acc_a = mfma_bf16<k32_layer<CINP>()>(wf[s], ba, acc_a);
+    acc_b = mfma_bf16<k32_layer<CINP>()>(wf[s], bb, acc_b);
     if (CHUNK > 0 && (s % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -180,12 +194,12 @@ __device__ __forceinline__ void conv_pair_bf3(const uint16_t* __restrict__ img, 
     const s8 hb = *reinterpret_cast<const s8*>(img + boff_b + off);
     const s8 la = *reinterpret_cast<const s8*>(img + boff_a + off + CINP);
     const s8 lb = *reinterpret_cast<const s8*>(img + boff_b + off + CINP);
-    acc_a = mfma_bf16(wl[s], ha, acc_a);
-    acc_b = mfma_bf16(wl[s], hb, acc_b);
-    acc_a = mfma_bf16(wh[s], la, acc_a);
-    acc_b = mfma_bf16(wh[s], lb, acc_b);
-    acc_a = mfma_bf16(wh[s], ha, acc_a);
-    acc_b = mfma_bf16(wh[s], hb, acc_b);
+    acc_a = mfma_bf16<k32_layer<CINP>()>(wl[s], ha, acc_a);
+    acc_b = mfma_bf16<k32_layer<CINP>()>(wl[s], hb, acc_b);
+    acc_a = mfma_bf16<k32_layer<CINP>()>(wh[s], la, acc_a);
+    acc_b = mfma_bf16<k32_layer<CINP>()>(wh[s], lb, acc_b);
+    acc_a = mfma_bf16<k32_layer<CINP>()>(wh[s], ha, acc_a);
+    acc_b = mfma_bf16<k32_layer<CINP>()>(wh[s], hb, acc_b);
     if (CHUNK > 0 && (s % CHUNK) == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
   }
 }
