@@ -59,13 +59,27 @@ __device__ __forceinline__ f2 w16(int e) {
   }
 }
 
+#ifdef WK_QTURN_PK
+// s * swap(v) as ONE v_pk_mul_f32 (the swap in op_sel, the signs in an SGPR
+// pair).  Left to itself the compiler builds swp(v) with two v_mov_b32 into
+// the halves of a register pair; with a K = 32 MFMA in flight on the same
+// SIMD, packed ops reading such a pair came out wrong in lanes 48-63
+// (the K = 32 question; tools/debug/xdl_coresidence_probe.hip).
+__device__ __forceinline__ f2 swap_mul(f2 v, f2 s) {
+  f2 r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(v), "s"(s));
+  return r;
+}
+#else
+__device__ __forceinline__ f2 swap_mul(f2 v, f2 s) { return swp(v) * s; }
+#endif
 // v * W16^e with the quarter turns folded (e is a constant after unrolling).
 __device__ __forceinline__ f2 twid16(f2 v, int e) {
   switch (e & 15) {
     case 0: return v;
-    case 4: return swp(v) * f2{1.0f, -1.0f};    // -i v
+    case 4: return swap_mul(v, f2{1.0f, -1.0f});    // -i v
     case 8: return -v;
-    case 12: return swp(v) * f2{-1.0f, 1.0f};   // i v
+    case 12: return swap_mul(v, f2{-1.0f, 1.0f});   // i v
     default: return cmulc(v, w16(e));
   }
 }

@@ -56,6 +56,11 @@ __device__ float* g_lmel_dbg;
 #endif
 constexpr int kProwClips = WK_PROW_CLIPS;
 #endif
+#ifdef WK_DIAG_FEDUMP
+// ... and the front-end registers of the same clips' frames at four points of
+// fe_rest ([grid * kProwClips][64 frames][4][16 lanes][32]; wk_fe_dev.h).
+__device__ float* g_fe_dump;
+#endif
 
 
 constexpr int NBF = 4;               // clips per CNN batch
@@ -316,7 +321,14 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       };
       WK_STAMP(1);
       float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
+#ifdef WK_DIAG_FEDUMP
+      float* fd = (i < kProwClips && fl < kNFramesB && g_fe_dump)
+                      ? g_fe_dump + ((size_t)(blockIdx.x * kProwClips + i) * 64 + fl) * 2048
+                      : nullptr;
+      fe_rest<true>(a, j, row, row + (fl & 1), tb, w0, tws, 0, pf_part WK_SP_ARG, fd);
+#else
       fe_rest<true>(a, j, row, row + (fl & 1), tb, w0, tws, 0, pf_part WK_SP_ARG);
+#endif
 #ifdef WK_DIAG_PROW
       if (i < kProwClips && fl < kNFramesB && g_prow_dbg) {   // snapshot A: this lane's bins as it wrote them
         float* dA = g_prow_dbg + ((size_t)(blockIdx.x * kProwClips + i) * 64 + fl) * 257;
@@ -838,6 +850,14 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
 #endif
   fe_init_tables<true, true>(smem, tid, kFusedBlock);
   for (int i = tid; i < kFusedLds - kGOff; i += kFusedBlock) smem[kGOff + i] = 0.0f;  // ctrl, guards, pads
+#ifdef WK_DIAG_K32_SPIN
+  // Diagnostic (K = 32 question; -DWK_DIAG builds, front-end-only
+  // mode): the CNN waves run a bare MFMA stream on register operands --
+  // WK_DIAG_K32_SPIN=1 the K = 32 bf16 form, 0 the K = 16 pair -- for as long
+  // as the front-end role runs, with no LDS traffic of their own.
+  __shared__ unsigned fe_done;
+  if (tid == 0) fe_done = 0;
+#endif
   __syncthreads();
   const int64_t n_mine = batch > (int64_t)blockIdx.x ? (batch - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   // The front-end role is the critical path: static issue priority over the
@@ -846,7 +866,28 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
   if (wave < 8) __builtin_amdgcn_s_setprio(kPrioFe);
   if (wave < 8) {
     if (!(diag & 2)) fe_role<T>(smem, audio, n_mine, clip_stride, feats_out, wave, lane, diag);
+#ifdef WK_DIAG_K32_SPIN
+    if (lane == 0) atomicAdd(&fe_done, 1u);
+#endif
   } else {
+#ifdef WK_DIAG_K32_SPIN
+    if (diag & 1) {
+      f32x4 acc[4] = {};
+      s8 a, b;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        a[q] = (short)(0x3c00 + ((lane + q) & 7));
+        b[q] = (short)(0x3c00 + ((3 * lane + q) & 7));
+      }
+      for (int n = 0; n < (1 << 22); n += 16) {   // bounded: ~4 M MFMAs at most
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j & 3] = mfma_bf16<WK_DIAG_K32_SPIN != 0>(a, b, acc[j & 3]);
+        if (__builtin_amdgcn_readfirstlane(*(volatile unsigned*)&fe_done) >= 8u) break;
+      }
+      if (feats_out) reinterpret_cast<f32x4*>(feats_out)[(size_t)blockIdx.x * 512 + (wave - 8) * 64 + lane] =
+          acc[0] + acc[1] + acc[2] + acc[3];   // (keeps the MFMAs; the feature output is not read in this mode)
+    }
+#endif
     if (!(diag & 1)) {
       LogmelSrc<CM, FEATS> src = {smem, reinterpret_cast<unsigned*>(smem + kCtrlOff), feats_out, (int64_t)blockIdx.x,
                                   (int64_t)gridDim.x, 0, 0, diag};
@@ -933,6 +974,11 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_cnn_fused_kernel(const floa
 
 
 
+#ifdef WK_DIAG_FEDUMP
+extern "C" int wk_debug_fe_buffer(void* d) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fe_dump), &d, sizeof(d)) != hipSuccess;
+}
+#endif
 #ifdef WK_DIAG_PROW
 extern "C" int wk_debug_prow_buffer(void* d) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_prow_dbg), &d, sizeof(d)) != hipSuccess;

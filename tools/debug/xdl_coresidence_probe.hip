@@ -44,6 +44,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kThreads = 1024, kValuWaves = 8, kChains = WK_PROBE_CHAINS;
+constexpr int kOutBlocks = 9;            // f32x4 outputs per VALU lane
 constexpr int kLdsFloats = 24 * 1024;   // ~96 KB: one workgroup per CU
 
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
@@ -70,6 +71,55 @@ __device__ __forceinline__ float dpp_shr1_keep(float old, float x) {   // row_sh
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, x),
                                                                0x111, 0xf, 0xf, false));
 }
+// The front-end's in-register DFT16 (wk_common.h: dft4 / twid16 / dft16, the
+// same packed-fp32 forms), restated here so the probe stays standalone.
+__device__ __forceinline__ f32x2 p_swp(f32x2 a) { return __builtin_shufflevector(a, a, 1, 0); }
+__device__ __forceinline__ f32x2 p_fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 p_twid(f32x2 v, int e) {
+  constexpr float c8 = 0.92387953251128674f, s8 = 0.38268343236508978f, h = 0.70710678118654752f;
+  const float W[16][2] = {{1.f, 0.f}, {c8, -s8}, {h, -h}, {s8, -c8}, {0.f, -1.f}, {-s8, -c8}, {-h, -h}, {-c8, -s8},
+                          {-1.f, 0.f}, {-c8, s8}, {-h, h}, {-s8, c8}, {0.f, 1.f}, {s8, c8}, {h, h}, {c8, s8}};
+  switch (e & 15) {
+    case 0: return v;
+    case 4: return p_swp(v) * f32x2{1.0f, -1.0f};
+    case 8: return -v;
+    case 12: return p_swp(v) * f32x2{-1.0f, 1.0f};
+    default: return p_fma2(p_swp(v), f32x2{-W[e & 15][1], W[e & 15][1]}, v * f32x2{W[e & 15][0], W[e & 15][0]});
+  }
+}
+__device__ __forceinline__ void p_dft4(f32x2& a0, f32x2& a1, f32x2& a2, f32x2& a3) {
+  const f32x2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = a1 - a3;
+  a0 = t0 + t2;
+  a2 = t0 - t2;
+  a1 = p_fma2(p_swp(t3), f32x2{1.0f, -1.0f}, t1);
+  a3 = p_fma2(p_swp(t3), f32x2{-1.0f, 1.0f}, t1);
+}
+// -i v as one packed op (the swap in op_sel, the sign from a {1, -1} constant):
+// the compiler's own form of p_twid(v, 4) is two v_mov_b32 (a register-pair
+// swap) with the sign folded into a later op.
+__device__ __forceinline__ f32x2 p_mul_negi_pk(f32x2 v) {
+  f32x2 r;
+  const f32x2 c = {1.0f, -1.0f};
+  asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(v), "v"(c));
+  return r;
+}
+template <int KA>
+__device__ __forceinline__ void p_rowgroup(f32x2 (&a)[16]) {
+#pragma unroll
+  for (int nb = 1; nb < 4; ++nb) a[4 * KA + nb] = p_twid(a[4 * KA + nb], nb * KA);
+  p_dft4(a[4 * KA], a[4 * KA + 1], a[4 * KA + 2], a[4 * KA + 3]);
+}
+__device__ __forceinline__ void p_dft16(f32x2 (&a)[16]) {
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) p_dft4(a[nb], a[4 + nb], a[8 + nb], a[12 + nb]);
+#pragma unroll
+  for (int ka = 1; ka < 4; ++ka)
+#pragma unroll
+    for (int nb = 1; nb < 4; ++nb) a[4 * ka + nb] = p_twid(a[4 * ka + nb], nb * ka);
+#pragma unroll
+  for (int ka = 0; ka < 4; ++ka) p_dft4(a[4 * ka], a[4 * ka + 1], a[4 * ka + 2], a[4 * ka + 3]);
+}
+
 __device__ __forceinline__ float dpp_mirror(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x140, 0xf, 0xf, false));
 }
@@ -79,7 +129,12 @@ __device__ __forceinline__ float dpp_mirror(float x) {
 // the split's row_mirror -> row_shr:1 (bound_ctrl off) pair; 2 = v_log_f32 /
 // v_exp_f32 and a lane select per iteration; 4 = the MFMA waves read their B
 // operand from LDS and store their accumulators to LDS (the CNN role's epilogue
-// stores), in their own LDS range.
+// stores), in their own LDS range; 32 = the VALU waves run the front-end's
+// in-register DFT16 instead of the rotations; 64 = one packed-fp32 form,
+// chosen by VAR >> 8: 0 v_pk_add_f32, 1 the same with neg (a subtract), 2
+// v_pk_fma_f32 with a swapped source and an SGPR-pair constant, 3 v_pk_mul_f32
+// by an SGPR constant's low half, 4 v_pk_fma_f32 with an SGPR-pair factor,
+// 5 v_pk_fma_f32 all-VGPR; +128: the 16 ops back to back on one chain.
 // 8 = each iteration adds a value loaded from global memory (a buffer load into
 // VGPRs, as the front-end's audio loads) and a 64-bit LDS table read (its
 // twiddles); 16 = the MFMA waves leave ~3/4 of their issue time idle
@@ -109,6 +164,119 @@ __global__ __launch_bounds__(kThreads) void probe_kernel(int iters, int VAR, con
     }
     float* my = lds + wave * 64 * 4;
     f32x2 sum = {0.0f, 0.0f};
+    f32x2 dd[16] = {};
+    if (VAR & 64) {   // one packed-fp32 instruction form, form = VAR >> 8 (16 independent chains)
+      const int form = VAR >> 8;
+      f32x2 d[16], y[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        d[q] = f32x2{0.01f * (float)((lane * 7 + q * 3 + blockIdx.x) % 29) - 0.14f, 0.01f * (float)((lane + q * 5) % 31) - 0.15f};
+        y[q] = f32x2{1e-4f * (float)((lane + q) % 13), -1e-4f * (float)((lane * 3 + q) % 11)};
+      }
+      const f32x2 ce = {0.00390625f, -0.00390625f}, cm = {-1.0f, 0.5f};
+      const bool dep = VAR & 128;   // 128: all 16 ops on chain 0, each reading the previous one's result
+      for (int it = 0; it < iters; ++it) {
+        if (form == 0) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) asm volatile("v_pk_add_f32 %0, %1, %2" : "=v"(d[dep ? 0 : q]) : "v"(d[dep ? 0 : q]), "v"(y[q]));
+        } else if (form == 1) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            asm volatile("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d[dep ? 0 : q]) : "v"(d[dep ? 0 : q]), "v"(y[q]));
+        } else if (form == 2) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1]" : "=v"(d[dep ? 0 : q]) : "v"(d[dep ? 0 : q]), "s"(ce), "v"(d[dep ? 0 : q]));
+        } else if (form == 3) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(d[dep ? 0 : q]) : "v"(d[dep ? 0 : q]), "s"(cm));
+        } else if (form == 4) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d[q]) : "v"(y[q]), "s"(cm), "v"(d[dep ? 0 : q]));
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d[dep ? 0 : q]) : "v"(d[dep ? 0 : q]), "v"(y[q]), "v"(d[dep ? 0 : q]));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sum += d[q];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dd[q] = d[q];
+    } else if (VAR & 32) {   // the front-end's DFT16, scaled by 1/4 per pass (norm-preserving)
+      f32x2 d[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        d[q] = f32x2{0.01f * (float)((lane * 7 + q * 3 + blockIdx.x) % 29) - 0.14f, 0.01f * (float)((lane + q * 5) % 31) - 0.15f};
+      const int sub = VAR >> 8;   // 0 the DFT16; 1 its two DFT4 passes without twiddles; 2 the twiddles only;
+                                  // 3 one DFT4 pass; 4 the DFT4 pass of rows only (no swapped operands: a0/a2 sums);
+                                  // 5 twiddles + the row pass; 6 the column pass + twiddles;
+                                  // 7-9 row group ka = sub - 6 alone (twiddles + DFT4);
+                                  // 10 sub 5 with the quarter turn as one packed op
+      for (int it = 0; it < iters; ++it) {
+        if (sub == 0) {
+          p_dft16(d);
+        } else if (sub == 1) {
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb) p_dft4(d[nb], d[4 + nb], d[8 + nb], d[12 + nb]);
+#pragma unroll
+          for (int ka = 0; ka < 4; ++ka) p_dft4(d[4 * ka], d[4 * ka + 1], d[4 * ka + 2], d[4 * ka + 3]);
+        } else if (sub == 2) {
+#pragma unroll
+          for (int ka = 1; ka < 4; ++ka)
+#pragma unroll
+            for (int nb = 1; nb < 4; ++nb) d[4 * ka + nb] = p_twid(d[4 * ka + nb], nb * ka);
+        } else if (sub == 5 || sub == 6) {   // 5: twiddles then the row DFT4 pass; 6: the column pass then the twiddles
+          if (sub == 6) {
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) p_dft4(d[nb], d[4 + nb], d[8 + nb], d[12 + nb]);
+          }
+#pragma unroll
+          for (int ka = 1; ka < 4; ++ka)
+#pragma unroll
+            for (int nb = 1; nb < 4; ++nb) d[4 * ka + nb] = p_twid(d[4 * ka + nb], nb * ka);
+          if (sub == 5) {
+#pragma unroll
+            for (int ka = 0; ka < 4; ++ka) p_dft4(d[4 * ka], d[4 * ka + 1], d[4 * ka + 2], d[4 * ka + 3]);
+          }
+        } else if (sub == 10) {   // sub 5 with the quarter-turn twiddle (ka 2, nb 2) as one packed op
+#pragma unroll
+          for (int ka = 1; ka < 4; ++ka)
+#pragma unroll
+            for (int nb = 1; nb < 4; ++nb)
+              d[4 * ka + nb] = (nb * ka == 4) ? p_mul_negi_pk(d[4 * ka + nb]) : p_twid(d[4 * ka + nb], nb * ka);
+#pragma unroll
+          for (int ka = 0; ka < 4; ++ka) p_dft4(d[4 * ka], d[4 * ka + 1], d[4 * ka + 2], d[4 * ka + 3]);
+        } else if (sub == 7) {   // one row group ka = sub - 6: its twiddles, then its DFT4
+          p_rowgroup<1>(d);
+        } else if (sub == 8) {
+          p_rowgroup<2>(d);
+        } else if (sub == 9) {
+          p_rowgroup<3>(d);
+        } else if (sub == 3) {
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb) p_dft4(d[nb], d[4 + nb], d[8 + nb], d[12 + nb]);
+        } else {
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb) {
+            const f32x2 t0 = d[nb] + d[8 + nb], t1 = d[nb] - d[8 + nb], t2 = d[4 + nb] + d[12 + nb], t3 = d[4 + nb] - d[12 + nb];
+            d[nb] = t0 + t2;
+            d[8 + nb] = t0 - t2;
+            d[4 + nb] = t1 + t3;
+            d[12 + nb] = t1 - t3;
+          }
+        }
+        const float sc = sub == 2 ? 1.0f : sub >= 3 ? 0.5f : 0.25f;   // (10 too)   // (5, 6: one pass, x 1/2)   // keeps the norm
+#pragma unroll
+        for (int q = 0; q < 16; ++q) d[q] *= f32x2{sc, sc};
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sum += d[q] * f32x2{(float)(q + 1), (float)(17 - q)};
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dd[q] = d[q];
+    } else
     for (int it = 0; it < iters; ++it) {
       if (!(VAR & 1)) {
 #pragma unroll
@@ -134,10 +302,15 @@ __global__ __launch_bounds__(kThreads) void probe_kernel(int iters, int VAR, con
       const float back = my[63 - lane];
       sum = pk_fma(f32x2{m, back}, f32x2{1.0f, 1.0f}, sum);
     }
-    f32x4* o = reinterpret_cast<f32x4*>(out) + ((size_t)blockIdx.x * kValuWaves + wave) * 64 * (kChains / 2 + 1);
+    f32x4* o = reinterpret_cast<f32x4*>(out) + ((size_t)blockIdx.x * kValuWaves + wave) * 64 * kOutBlocks;
+    if (VAR & 96) {   // the 16 complex registers, then the weighted sum
 #pragma unroll
-    for (int k = 0; k < kChains; k += 2) o[(k / 2) * 64 + lane] = f32x4{v[k].x, v[k].y, v[k + 1].x, v[k + 1].y};
-    o[(kChains / 2) * 64 + lane] = f32x4{sum.x, sum.y, 0.0f, 0.0f};
+      for (int k = 0; k < 16; k += 2) o[(k / 2) * 64 + lane] = f32x4{dd[k].x, dd[k].y, dd[k + 1].x, dd[k + 1].y};
+    } else {
+#pragma unroll
+      for (int k = 0; k < kChains && k < 16; k += 2) o[(k / 2) * 64 + lane] = f32x4{v[k].x, v[k].y, v[k + 1].x, v[k + 1].y};
+    }
+    o[8 * 64 + lane] = f32x4{sum.x, sum.y, 0.0f, 0.0f};
     __builtin_amdgcn_s_waitcnt(0);
     if (lane == 0) atomicAdd(&done, 1u);
   } else {
@@ -205,7 +378,7 @@ int main(int argc, char** argv) {
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int grid = cus;
-  const size_t nv = (size_t)grid * kValuWaves * 64 * (kChains / 2 + 1) * 4, nm = (size_t)grid * 8 * 64 * 4;
+  const size_t nv = (size_t)grid * kValuWaves * 64 * kOutBlocks * 4, nm = (size_t)grid * 8 * 64 * 4;
   float *d_out, *d_m;
   unsigned* d_info;
   CHECK(hipMalloc(&d_out, nv * 4));
@@ -248,18 +421,22 @@ int main(int argc, char** argv) {
     for (int r = 0; r < reps; ++r) {
       const float ms = launch(mode);
       long diff = 0;
-      int hist[64] = {};
-      const size_t per_wave = 64 * (kChains / 2 + 1) * 4;
+      int hist[64] = {}, slot[64] = {};
+      const size_t per_wave = 64 * kOutBlocks * 4;
       for (size_t i = 0; i < nv; ++i)
         if (memcmp(&got[i], &ref[i], 4) != 0) {
           ++diff;
           hist[(i % per_wave) / 4 % 64]++;
+          slot[((i % per_wave) / 256) * 4 + (i % 4)]++;   // the lane's output float: d[q].x/.y (float 2q, 2q + 1), then sum.x, sum.y at 32, 33
         }
       printf("mode %-14s rep %d: %.3f ms, differing values %ld", names[mode], r, ms, diff);
       if (diff) {
         printf("; by lane:");
         for (int l = 0; l < 64; ++l)
           if (hist[l]) printf(" %d:%d", l, hist[l]);
+        printf("; by output float:");
+        for (int l = 0; l < 4 * kOutBlocks; ++l)
+          if (slot[l]) printf(" %d:%d", l, slot[l]);
       }
       printf("\n");
       fflush(stdout);
