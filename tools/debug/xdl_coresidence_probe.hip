@@ -124,7 +124,8 @@ __device__ __forceinline__ float dpp_mirror(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x140, 0xf, 0xf, false));
 }
 
-// MODE 0: no MFMA stream, 1: K = 16 bf16 pair, 2: K = 32 bf16, 3: K = 32 f16.
+// MODE 0: no MFMA stream, 1: K = 16 bf16 pair, 2: K = 32 bf16, 3: K = 32 f16,
+// 4-6 K = 32 bf16 with A/B, everything, or the accumulator in AGPRs (XDL_PROBE_ALL_MODES=1).
 // VAR bits (0 = VGPR constants, row_mirror only): 1 = SGPR-pair constants and
 // the split's row_mirror -> row_shr:1 (bound_ctrl off) pair; 2 = v_log_f32 /
 // v_exp_f32 and a lane select per iteration; 4 = the MFMA waves read their B
@@ -343,6 +344,12 @@ __global__ __launch_bounds__(kThreads) void probe_kernel(int iters, int VAR, con
           } else if (MODE == 2) {
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                         0, 0, 0);
+          } else if (MODE == 4) {   // K = 32 bf16, A and B operands in AGPRs
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "a"(a), "a"(b));
+          } else if (MODE == 5) {   // K = 32 bf16, A, B and the accumulator in AGPRs
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "a"(a), "a"(b));
+          } else if (MODE == 6) {   // K = 32 bf16, the accumulator in AGPRs, A and B in VGPRs
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
           } else {
             c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
                                                        0, 0);
@@ -368,7 +375,10 @@ static void launch_mode(int mode, int var, int grid, int iters, const float* tab
     case 0: hipLaunchKernelGGL(probe_kernel<0>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
     case 1: hipLaunchKernelGGL(probe_kernel<1>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
     case 2: hipLaunchKernelGGL(probe_kernel<2>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
-    default: hipLaunchKernelGGL(probe_kernel<3>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
+    case 3: hipLaunchKernelGGL(probe_kernel<3>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
+    case 4: hipLaunchKernelGGL(probe_kernel<4>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
+    case 5: hipLaunchKernelGGL(probe_kernel<5>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
+    default: hipLaunchKernelGGL(probe_kernel<6>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
   }
 }
 
@@ -416,8 +426,9 @@ int main(int argc, char** argv) {
            cnt[1][0], cnt[1][1], cnt[2][0], cnt[2][1], cnt[3][0], cnt[3][1]);
   }
   printf("valu variant %d, %d iterations\n", var, iters);
-  const char* names[4] = {"none", "k16_bf16_pair", "k32_bf16", "k32_f16"};
-  for (int mode = 0; mode < 4; ++mode) {
+  const char* names[7] = {"none", "k16_bf16_pair", "k32_bf16", "k32_f16", "k32_ab_agpr", "k32_all_agpr", "k32_acc_agpr"};
+  const int n_modes = getenv("XDL_PROBE_ALL_MODES") ? 7 : 4;
+  for (int mode = 0; mode < n_modes; ++mode) {
     for (int r = 0; r < reps; ++r) {
       const float ms = launch(mode);
       long diff = 0;
