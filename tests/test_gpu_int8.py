@@ -43,3 +43,22 @@ def test_int8_mfma_bit_exact_at_scale(m8, xiaoa_sd):
     got = m8(feats).reshape(-1).cpu().numpy()
     want = O.kws_forward_int8(O.quantize_input(feats), O.quantize_int8(xiaoa_sd)) * 0.125
     np.testing.assert_array_equal(got, want.astype(np.float32))
+
+
+def test_int8_mfma_repeatable_at_scale(m8, xiaoa_sd):
+    """65,536 clips of wide-range features through the int8 matrix-core kernel,
+    three launches, bit for bit; and a strided sample of 512 clips equal to
+    the oracle's integer network.  v_mfma_i32_16x16x64_i8 is one of the forms
+    that change co-resident packed-fp32 VALU results (DESIGN 5.1, K = 32):
+    this kernel's own VALU work is integer requantisation, and this test is
+    the at-scale check that it stays exact."""
+    import torch
+    g = torch.Generator().manual_seed(11)
+    feats = (4.0 * torch.randn((65536, 13, 63), generator=g)).cuda()
+    ref = m8(feats).reshape(-1).clone()
+    for _ in range(2):
+        assert torch.equal(m8(feats).reshape(-1), ref)
+    idx = np.arange(0, 65536, 128)
+    f_s = feats[torch.from_numpy(idx).cuda()].cpu().numpy()
+    want = O.kws_forward_int8(O.quantize_input(f_s), O.quantize_int8(xiaoa_sd)) * 0.125
+    np.testing.assert_array_equal(ref.cpu().numpy()[idx], want.astype(np.float32))

@@ -125,7 +125,8 @@ __device__ __forceinline__ float dpp_mirror(float x) {
 }
 
 // MODE 0: no MFMA stream, 1: K = 16 bf16 pair, 2: K = 32 bf16, 3: K = 32 f16,
-// 4-6 K = 32 bf16 with A/B, everything, or the accumulator in AGPRs (XDL_PROBE_ALL_MODES=1).
+// 4-6 K = 32 bf16 with A/B, everything, or the accumulator in AGPRs, 7 the fp32
+// v_mfma_f32_16x16x4_f32, 8 the int8 v_mfma_i32_16x16x64_i8 (XDL_PROBE_MODES="0278" etc.).
 // VAR bits (0 = VGPR constants, row_mirror only): 1 = SGPR-pair constants and
 // the split's row_mirror -> row_shr:1 (bound_ctrl off) pair; 2 = v_log_f32 /
 // v_exp_f32 and a lane select per iteration; 4 = the MFMA waves read their B
@@ -344,6 +345,13 @@ __global__ __launch_bounds__(kThreads) void probe_kernel(int iters, int VAR, con
           } else if (MODE == 2) {
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                         0, 0, 0);
+          } else if (MODE == 7) {   // the product's fp32 form, v_mfma_f32_16x16x4_f32 (fp32 convolutions)
+            c = __builtin_amdgcn_mfma_f32_16x16x4f32(__builtin_bit_cast(float, (int)a[0] << 16),
+                                                     __builtin_bit_cast(float, (int)b[0] << 16), c, 0, 0, 0);
+          } else if (MODE == 8) {   // the int8 K = 64 form, v_mfma_i32_16x16x64_i8 (wk_int8.hip)
+            typedef int i32x4 __attribute__((ext_vector_type(4)));
+            c = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, a), __builtin_bit_cast(i32x4, b),
+                                                                                __builtin_bit_cast(i32x4, c), 0, 0, 0));
           } else if (MODE == 4) {   // K = 32 bf16, A and B operands in AGPRs
             asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "a"(a), "a"(b));
           } else if (MODE == 5) {   // K = 32 bf16, A, B and the accumulator in AGPRs
@@ -378,7 +386,9 @@ static void launch_mode(int mode, int var, int grid, int iters, const float* tab
     case 3: hipLaunchKernelGGL(probe_kernel<3>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
     case 4: hipLaunchKernelGGL(probe_kernel<4>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
     case 5: hipLaunchKernelGGL(probe_kernel<5>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
-    default: hipLaunchKernelGGL(probe_kernel<6>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
+    case 6: hipLaunchKernelGGL(probe_kernel<6>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
+    case 7: hipLaunchKernelGGL(probe_kernel<7>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
+    default: hipLaunchKernelGGL(probe_kernel<8>, dim3(grid), dim3(kThreads), 0, 0, iters, var, table, out, m, info); break;
   }
 }
 
@@ -426,9 +436,11 @@ int main(int argc, char** argv) {
            cnt[1][0], cnt[1][1], cnt[2][0], cnt[2][1], cnt[3][0], cnt[3][1]);
   }
   printf("valu variant %d, %d iterations\n", var, iters);
-  const char* names[7] = {"none", "k16_bf16_pair", "k32_bf16", "k32_f16", "k32_ab_agpr", "k32_all_agpr", "k32_acc_agpr"};
-  const int n_modes = getenv("XDL_PROBE_ALL_MODES") ? 7 : 4;
-  for (int mode = 0; mode < n_modes; ++mode) {
+  const char* names[9] = {"none",         "k16_bf16_pair", "k32_bf16",      "k32_f16",      "k32_ab_agpr",
+                          "k32_all_agpr", "k32_acc_agpr",  "f32_16x16x4",   "i8_16x16x64"};
+  const char* sel = getenv("XDL_PROBE_MODES");   // e.g. "0127": the modes to run (default 0-3)
+  for (int mode = 0; mode < 9; ++mode) {
+    if (sel ? !strchr(sel, '0' + mode) : mode > 3) continue;
     for (int r = 0; r < reps; ++r) {
       const float ms = launch(mode);
       long diff = 0;
