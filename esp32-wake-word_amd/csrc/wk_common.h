@@ -15,12 +15,43 @@ constexpr int kFeBlock = 512;        // 8 waves per front-end workgroup
 // complex arithmetic then compiles to packed fp32 VALU (v_pk_add/mul/fma_f32,
 // two lanes' worth of fp32 per issue), swaps and sign flips folded into the
 // op_sel / neg modifiers.
+// Diagnostic builds (and -DWK_FE_PACKED_ALL, the A/B baseline) compile the
+// whole fused kernel in one translation unit (wk_fused.hip), with the packed
+// front-end in every precision.
+#if defined(WK_DIAG) || defined(WK_DIAG_PROW) || defined(WK_DIAG_FEDUMP) || defined(WK_DIAG_SIMD_SPLIT) || \
+    defined(WK_DIAG_K32_SPIN) || defined(WK_MFMA_K32) || defined(WK_FE_PACKED_ALL)
+#define WK_FUSED_ONE_TU 1
+#else
+#define WK_FUSED_ONE_TU 0
+#endif
+
+#if defined(WK_FE_SCALAR) && defined(WK_FUSED_TU)
+// The fused kernel's bf16-family unit (wk_fused_xdl.hip): the same complex
+// arithmetic as scalar fp32 pairs (v_fma/v_add/v_mul_f32; swaps and signs are
+// register choices and VOP3 neg modifiers), no packed ops -- beside the bf16
+// MFMAs those issue faster (wk_fused.hip header).
+struct __attribute__((aligned(8))) f2 {
+  float x, y;
+};
+__device__ __forceinline__ f2 operator+(f2 a, f2 b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ f2 operator-(f2 a, f2 b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ f2 operator*(f2 a, f2 b) { return {a.x * b.x, a.y * b.y}; }
+__device__ __forceinline__ f2 operator-(f2 a) { return {-a.x, -a.y}; }
+__device__ __forceinline__ f2& operator+=(f2& a, f2 b) { return a = a + b; }
+__device__ __forceinline__ f2& operator-=(f2& a, f2 b) { return a = a - b; }
+__device__ __forceinline__ f2& operator*=(f2& a, f2 b) { return a = a * b; }
+__device__ __forceinline__ f2 swp(f2 a) { return {a.y, a.x}; }
+__device__ __forceinline__ f2 bx(f2 a) { return {a.x, a.x}; }
+__device__ __forceinline__ f2 by(f2 a) { return {a.y, a.y}; }
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return {__builtin_fmaf(a.x, b.x, c.x), __builtin_fmaf(a.y, b.y, c.y)}; }
+#else
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 swp(f2 a) { return __builtin_shufflevector(a, a, 1, 0); }
 __device__ __forceinline__ f2 bx(f2 a) { return __builtin_shufflevector(a, a, 0, 0); }
 __device__ __forceinline__ f2 by(f2 a) { return __builtin_shufflevector(a, a, 1, 1); }
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+#endif
 __device__ __forceinline__ f2 sub_ib(f2 a, f2 b) { return fma2(swp(b), f2{1.0f, -1.0f}, a); }  // a - i b
 __device__ __forceinline__ f2 add_ib(f2 a, f2 b) { return fma2(swp(b), f2{-1.0f, 1.0f}, a); }  // a + i b
 
@@ -28,6 +59,9 @@ __device__ __forceinline__ f2 add_ib(f2 a, f2 b) { return fma2(swp(b), f2{-1.0f,
 // operand is w swizzled to {-s, s} by op_sel/neg_lo (the compiler would
 // build that pair with two extra VALU ops).
 __device__ __forceinline__ f2 cmul2(f2 a, f2 w) {
+#if defined(WK_FE_SCALAR) && defined(WK_FUSED_TU)
+  return {__builtin_fmaf(-a.y, w.y, a.x * w.x), __builtin_fmaf(a.x, w.y, a.y * w.x)};
+#endif
   const f2 t = a * bx(w);
   f2 r;
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
@@ -59,7 +93,7 @@ __device__ __forceinline__ f2 w16(int e) {
   }
 }
 
-#ifdef WK_QTURN_PK
+#if defined(WK_QTURN_PK) && !(defined(WK_FE_SCALAR) && defined(WK_FUSED_TU))
 // s * swap(v) as ONE v_pk_mul_f32 (the swap in op_sel, the signs in an SGPR
 // pair).  Left to itself the compiler builds swp(v) with two v_mov_b32 into
 // the halves of a register pair; with a K = 32 MFMA in flight on the same

@@ -18,12 +18,23 @@
 // different waves, so the roles overlap on every SIMD (2 front-end + 2 CNN
 // waves per SIMD), and features never touch HBM: per clip the kernel reads
 // its 64,000 audio bytes and writes one 4-byte logit.
+//
+// Product builds compile this file twice.  Here: the fp32 convolutions, with
+// the front-end's complex arithmetic as packed fp32 (v_pk_*_f32).  Through
+// wk_fused_xdl.hip (WK_FUSED_XDL_TU): the bf16 / bf16x3 convolutions, with the
+// same front-end as scalar fp32 pairs (WK_FE_SCALAR, wk_common.h).  Beside the
+// bf16 MFMAs, which run on the matrix pipe, packed fp32 issues slower than
+// scalar: +4.8 % bf16.  Beside the fp32 MFMAs, which share the fp32
+// datapath, scalar is 2.8 % slower (profiles/r05au_*).
+// Diagnostic builds (WK_FUSED_ONE_TU) keep every precision here.
+#define WK_FUSED_TU   // (wk_common.h: WK_FE_SCALAR applies to the fused translation units only)
 #include "wk_cnn_dev.h"
 #include "wk_fe_dev.h"
 #include "wk_kernels.h"
 
 using namespace wk;
 
+#if !(defined(WK_FUSED_XDL_TU) && WK_FUSED_ONE_TU)   // (the XDL unit is empty in diagnostic builds)
 namespace {
 
 #ifdef WK_DIAG
@@ -972,8 +983,7 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_cnn_fused_kernel(const floa
 
 }  // namespace
 
-
-
+#ifndef WK_FUSED_XDL_TU
 #ifdef WK_DIAG_FEDUMP
 extern "C" int wk_debug_fe_buffer(void* d) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_fe_dump), &d, sizeof(d)) != hipSuccess;
@@ -1005,15 +1015,28 @@ extern "C" int wk_debug_stamps(unsigned long long* host_out, int reset) {
 }
 #endif
 
+#endif   // !WK_FUSED_XDL_TU
+
 namespace wk {
 
+#ifdef WK_FUSED_XDL_TU
+hipError_t launch_fused_xdl(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
+                            const uint16_t* wbf, int conv_mode, float* logits, float* feats_or_null, int grid_cap,
+                            hipStream_t stream, unsigned* err, int diag) {
+#else
 hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
                         const uint16_t* wbf, int conv_mode, float* logits, float* feats_or_null, int grid_cap,
                         hipStream_t stream, unsigned* err, int diag) {
+#endif
   if (batch == 0) return hipSuccess;
   const int grid = (int)(batch < grid_cap ? batch : grid_cap);
   const dim3 g(grid), blk(kFusedBlock);
   if (conv_mode != kConvF32 && !wbf) return hipErrorInvalidValue;
+#if !WK_FUSED_ONE_TU && !defined(WK_FUSED_XDL_TU)
+  if (conv_mode != kConvF32)   // the bf16 family: wk_fused_xdl.hip (scalar-fp32 front-end)
+    return launch_fused_xdl(i16, audio, batch, clip_stride, w, wbf, conv_mode, logits, feats_or_null, grid_cap, stream,
+                            err, diag);
+#endif
 #define WK_FUSED_LAUNCH(T, CM)                                                                              \
   do {                                                                                                         \
     if (feats_or_null)                                                                                         \
@@ -1023,6 +1046,18 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
       hipLaunchKernelGGL((wk_fused_kernel<T, CM, false>), g, blk, 0, stream, (const T*)audio, batch,            \
                          clip_stride, w, wbf, logits, nullptr, err, diag);                                        \
   } while (0)
+#if defined(WK_FUSED_XDL_TU)   // bf16 / bf16x3 only
+  if (i16) {
+    if (conv_mode == kConvBf16x3) WK_FUSED_LAUNCH(int16_t, kConvBf16x3);
+    else WK_FUSED_LAUNCH(int16_t, kConvBf16);
+  } else {
+    if (conv_mode == kConvBf16x3) WK_FUSED_LAUNCH(float, kConvBf16x3);
+    else WK_FUSED_LAUNCH(float, kConvBf16);
+  }
+#elif !WK_FUSED_ONE_TU   // fp32 only (the bf16 family returned above)
+  if (i16) WK_FUSED_LAUNCH(int16_t, kConvF32);
+  else WK_FUSED_LAUNCH(float, kConvF32);
+#else
   if (i16) {
     if (conv_mode == kConvBf16) WK_FUSED_LAUNCH(int16_t, kConvBf16);
     else if (conv_mode == kConvBf16x3) WK_FUSED_LAUNCH(int16_t, kConvBf16x3);
@@ -1032,9 +1067,12 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
     else if (conv_mode == kConvBf16x3) WK_FUSED_LAUNCH(float, kConvBf16x3);
     else WK_FUSED_LAUNCH(float, kConvF32);
   }
+#endif
 #undef WK_FUSED_LAUNCH
   return hipGetLastError();
 }
+
+#ifndef WK_FUSED_XDL_TU
 
 hipError_t launch_cnn_fused(const float* feats, int64_t batch, const float* w, const uint16_t* wbf, int conv_mode,
                             float* logits, int grid_cap, hipStream_t stream, unsigned* err) {
@@ -1053,5 +1091,7 @@ hipError_t launch_cnn_fused(const float* feats, int64_t batch, const float* w, c
                        logits, err);
   return hipGetLastError();
 }
+#endif   // !WK_FUSED_XDL_TU
 
 }  // namespace wk
+#endif   // !(WK_FUSED_XDL_TU && WK_FUSED_ONE_TU)

@@ -44,6 +44,12 @@ hipError_t launch_fused(bool i16, const void* audio, int64_t batch, int64_t clip
                         int diag = 0);   // role isolation (-DWK_DIAG builds only): 1 = FE role only,
                                          // 2 = CNN role only; wrong logits
 
+// The bf16-family half of launch_fused (wk_fused_xdl.hip: conv_mode 1 / 2,
+// scalar-fp32 front-end); launch_fused calls it.
+hipError_t launch_fused_xdl(bool i16, const void* audio, int64_t batch, int64_t clip_stride, const float* w,
+                            const uint16_t* wbf, int conv_mode, float* logits, float* feats_or_null, int grid_cap,
+                            hipStream_t stream, unsigned* err, int diag);
+
 // CNN on caller features (wk_fused.hip, the fused kernel's CNN role fed from
 // HBM): feats [B][13][63] -> logits [B]; conv_mode as launch_fused.
 hipError_t launch_cnn_fused(const float* feats, int64_t batch, const float* w, const uint16_t* wbf, int conv_mode,

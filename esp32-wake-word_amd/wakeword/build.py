@@ -23,7 +23,7 @@ LIB = os.path.join(PKG, "libwakeword.so")
 HOST_LIB = os.path.join(PKG, "libwakeword_host.so")      # the host-CPU library (wk_host.cpp, no HIP)
 HOST_SOURCES = ["wk_host.cpp", "wk_wav.cpp"]   # (wk_wav.cpp is host C++ in both libraries)
 OBJDIR = os.path.join(ROOT, "build")
-SOURCES = ["wk_frontend.hip", "wk_fused.hip", "wk_misc.hip", "wk_api.hip", "wk_ctc.hip", "wk_wav.cpp", "wk_int8.hip", "wk_esp_mfcc.hip"]
+SOURCES = ["wk_frontend.hip", "wk_fused.hip", "wk_fused_xdl.hip", "wk_misc.hip", "wk_api.hip", "wk_ctc.hip", "wk_wav.cpp", "wk_int8.hip", "wk_esp_mfcc.hip"]
 LIBS = ["-Wl,-rpath,/opt/rocm/lib"]   # HIP runtime only: every GEMM is a hand-written kernel (no rocBLAS)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WK_OFFLOAD_ARCH", "gfx950")
