@@ -80,6 +80,12 @@ typedef short s8 __attribute__((ext_vector_type(8)));   // one lane's A or B fra
 #if defined(WK_MFMA_K32) && !defined(WK_ALLOW_K32_DIAG)
 #error "WK_MFMA_K32 corrupts the fused kernel's front-end (DESIGN.md 5.1); diagnostic builds add -DWK_ALLOW_K32_DIAG"
 #endif
+// Product (split) builds use the K = 32 form: the bf16-family fused unit's
+// front-end is scalar fp32, and the standalone CNN has none (k32_layer).
+// -DWK_XDL_K32_OFF keeps the K = 16 pair for A/B.
+#if !defined(WK_XDL_K32_OFF) && !defined(WK_XDL_K32)
+#define WK_XDL_K32 1
+#endif
 #ifndef WK_K32_MASK
 #define WK_K32_MASK 7   // diagnostic K = 32 builds: which conv layers use it (bit 0 conv1, 1 conv2, 2 conv3)
 #endif
@@ -108,8 +114,14 @@ __device__ __forceinline__ f32x4 mfma_bf16(s8 a, s8 b, f32x4 c) {
 // the conv layer of a CINP (16: conv1, 32: conv2, 64: conv3) uses the K = 32 form
 template <int CINP>
 constexpr bool k32_layer() {
-#ifdef WK_MFMA_K32
+#if defined(WK_MFMA_K32)
   return (WK_K32_MASK >> (CINP == 16 ? 0 : CINP == 32 ? 1 : 2)) & 1;
+#elif defined(WK_XDL_K32) && !WK_FUSED_ONE_TU
+  // Split product build: the bf16 convolutions run in the bf16-family fused
+  // unit, whose front-end has no packed fp32 (beside which the K = 32 form is
+  // exact), and in the standalone CNN kernel, which has no
+  // front-end; both use it, so the two accumulate alike.
+  return true;
 #else
   return false;
 #endif
