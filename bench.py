@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for the start/stop barriers and the max-over-ranks time (nccl = "
                          "RCCL over xGMI; gloo lets several ranks share one GPU for a rehearsal of the N>1 path)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the config 4 / 5 / 3 measurements added to the line after the headline (N=1 only)")
     ap.add_argument("--precision", default="fp32", choices=list(PRECISIONS),
                     help="CNN convolutions: fp32 MFMA (config 2, default), bf16 (config 4), or bf16x3 "
                          "(config 2 at fp32-grade accuracy on split-bf16 MFMA); front-end fp32 always")
@@ -201,6 +203,83 @@ def cpu_baseline(seconds: float, batches=CPU_BATCHES):
             "sample": "; ".join(parts) + " (synthetic clips, seed 1234); torch-CPU fp32 restatement of the "
                       "torchaudio MFCC+CMVN front-end + LightweightKWS on the xiaoa.onnx weights "
                       f"(oracle/wk_torch_cpu.py), torch.set_num_threads({threads})"}
+
+
+CONFIG4_CLIPS = 131_072   # 1,048,576 clips over 8 GPUs = 131,072 per rank
+HBM_ROOF_F32_WPS = PEAK_HBM_GBS * 1e9 / BYTES_PER_WINDOW_F32   # 125.0 M windows/s with fp32 audio
+
+
+def extra_config4(torch, wakeword, _lib, local, seed, steps=10, warmup=2):
+    """Config 4 on this GPU: one rank's share (131,072 clips) through the fused
+    kernel with bf16 convolutions, fp32 audio resident in HBM.  Its governing
+    roof is HBM (125 M windows/s with fp32 input); the blended
+    compute ceiling of roofline_peak("bf16") is listed beside it."""
+    B = CONFIG4_CLIPS
+    model = wakeword.load_onnx(os.path.join(REPO, "tests", "golden", "xiaoa.onnx"), device=local, precision="bf16")
+    clips = wakeword.synth_clips(seed, 0, B, 16000, device=local)
+    logits = torch.empty((B,), dtype=torch.float32, device=f"cuda:{local}")
+    L = _lib.lib()
+    stream = torch.cuda.current_stream(local)
+    sptr = C.c_void_p(stream.cuda_stream)
+
+    def step():
+        _lib.check(L.wk_forward(model._h.h, C.c_void_p(clips.data_ptr()), _lib.WK_DTYPE_F32, B, 16000, 16000,
+                                C.c_void_p(logits.data_ptr()), None, sptr), "wk_forward")
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    flags = C.c_uint32(0)
+    _lib.check(L.wk_check_device_errors(model._h.h, C.byref(flags)), "wk_check_device_errors")
+    ok = flags.value == 0 and bool(torch.isfinite(logits).all())
+    value = B * steps / el
+    gbs = BYTES_PER_WINDOW_F32 * B / (launch_ms * 1e-3) / 1e9
+    peak_c, basis_c = roofline_peak("bf16")
+    achieved_c = FLOP_PER_WINDOW * B / (launch_ms * 1e-3) / 1e12
+    del clips
+    return {"workload": "config4: fused MFCC(torchaudio+CMVN) fp32 + xiaoa CNN bf16, one rank's share of "
+                        "1,048,576 clips (131,072), fp32 audio resident in HBM",
+            "value": round(value, 1), "unit": "windows/s per GPU", "batch_per_gpu": B, "steps": steps,
+            "warmup": warmup, "ms_per_step": round(el / steps * 1e3, 4), "dtype": PRECISIONS["bf16"][0],
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(gbs / PEAK_HBM_GBS, 4), "launch_ms": round(launch_ms, 4),
+                         "windows_per_s_roof": round(HBM_ROOF_F32_WPS, 1)},
+            "compute_ceiling": {"achieved": round(achieved_c, 3), "peak": round(peak_c, 1), "unit": "TFLOP/s",
+                                "frac": round(achieved_c / peak_c, 4), "basis": basis_c},
+            "logits_finite_and_no_device_error": ok}
+
+
+def extra_config5(local):
+    """Config 5 (bench_ctc.run_ctc): CTC head, B = 4096 utterances of 3 s, V = 4000, fp16."""
+    import bench_ctc
+    line = bench_ctc.run_ctc(batch=4096, vocab=4000, seconds=3, steps=5, warmup=1, precision="fp16", device=local)
+    k = line["kernels"]
+    return {"workload": line["config"]["workload"] + f", B = 4096, V = 4000, T = {line['config']['T']}, fp16",
+            "value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
+            "steps": line["steps"], "warmup": line["warmup"], "dtype": line["dtype"],
+            "call": line["config"]["call"], "roofline": line["roofline"],
+            "output_kernel": {x: k["output"][x] for x in ("ms", "achieved", "peak", "unit", "frac")}
+            if "output" in k else None,
+            "stages": {s: {"ms": v["ms"], "frac": v["frac"], "bound": v["bound"]} for s, v in k.items()},
+            "data": line["data"]}
+
+
+def extra_config3(wakeword, local):
+    """Config 3 (bench_stream.run_stream): 60 s stream pushed hop by hop (30 ms), p50 push -> logit on
+    the host; throughput of a 1 h resident backlog."""
+    import bench_stream
+    line = bench_stream.run_stream(60, 480, 3600, device=local)
+    line.pop("metric", None)
+    line["workload"] = "config3: streaming 1 s windows at 30 ms hop, fp32, batch 1 per push"
+    return line
 
 
 def load_traffic(precision="fp32"):
@@ -368,6 +447,16 @@ def main():
             out["roofline"]["traffic_source"] = traffic_src
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if world == 1 and not shared and not args.no_extras:
+            # SURVEY 8(d) configs 4, 5, 3, measured after the headline's timed
+            # region and its CPU leg (the headline above is unchanged by them)
+            del clips
+            torch.cuda.empty_cache()
+            out["config4"] = extra_config4(torch, wakeword, _lib, local, args.seed)
+            torch.cuda.empty_cache()
+            out["config5"] = extra_config5(local)
+            torch.cuda.empty_cache()
+            out["config3"] = extra_config3(wakeword, local)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

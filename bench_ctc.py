@@ -69,62 +69,57 @@ def load_traffic(tag):
         return {}, None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=4096)
-    ap.add_argument("--vocab", type=int, default=4000)
-    ap.add_argument("--seconds", type=int, default=3)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--cpu-utts", type=int, default=128)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16"],
-                    help="GEMM operand precision (config 5 names fp16; fp32 is the parity mode)")
-    ap.add_argument("--separate", action="store_true",
-                    help="time wk_ctc_features + wk_ctc_forward instead of the one-call wk_ctc_transcribe")
-    args = ap.parse_args()
+def run_ctc(batch=4096, vocab=4000, seconds=3, steps=5, warmup=1, precision="fp16", separate=False, device=0,
+            keep=None):
+    """Config 5 on the HIP path: the timed steps, then the per-stage profile.
+    Returns the JSON line's dict (no CPU baseline).  Weights are seeded
+    random GRU_CTC_Model weights (wakeword.ctc.random_state_dict: the
+    reference ships none).  keep: optional dict that receives the model and
+    the audio (the CPU-baseline leg reuses them)."""
     import torch
     import wakeword
     from wakeword import _lib
-    from oracle import wk_ctc_oracle as CO
+    from wakeword.ctc import random_state_dict
 
-    f16 = args.precision == "fp16"
-    n = args.seconds * 16000
+    f16 = precision == "fp16"
+    n = seconds * 16000
     T = 1 + n // 160
-    B, V = args.batch, args.vocab
-    m = CO.make_model(V, seed=0)
-    g = wakeword.CTCModel(m.state_dict(), V, precision=args.precision)
-    audio = wakeword.synth_clips(1234, 0, B, n)
-    if args.separate:
+    B, V = batch, vocab
+    sd = random_state_dict(V, seed=0)
+    g = wakeword.CTCModel(sd, V, device=device, precision=precision)
+    audio = wakeword.synth_clips(1234, 0, B, n, device=device)
+    if keep is not None:
+        keep.update(state_dict=sd, audio=audio)
+    if separate:
         def step():
             tok, ln, _ = g.decode(g.features(audio, n_samples=n))
             return tok, ln
     else:
         def step():
             return g.decode_audio(audio, n_samples=n)
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
 
     # timed region: the whole step, host clock, no per-stage events
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         tok, ln = step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    value = B * args.steps / el
+    value = B * steps / el
     assert int(ln.min()) >= 0 and int(ln.max()) <= T
 
     # per-stage durations: the same steps again with HIP events around each stage
     L = _lib.lib()
     _lib.check(L.wk_ctc_profile(g._h, 1), "wk_ctc_profile")
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     ms = (C.c_double * len(STAGES))()
     cnt = (C.c_int64 * len(STAGES))()
     _lib.check(L.wk_ctc_stage_times(g._h, ms, cnt), "wk_ctc_stage_times")
     _lib.check(L.wk_ctc_profile(g._h, 0), "wk_ctc_profile")
-    zfold = f16 and not args.separate and T >= 6
+    zfold = f16 and not separate and T >= 6
     work = stage_work(B, T, V, n, f16, zfold)
     fused = f16 and cnt[STAGES.index("proj0")] == 0
     if fused:
@@ -142,7 +137,7 @@ def main():
             by_g, fl_g = work[f"gru{l}"]
             by_p, fl_p = work[f"proj{l}"]
             work[f"gru{l}"] = (2 * rows * din * 2 + rows * 2 * H * 2 + 6 * H * din * 2, fl_g + fl_p)
-    traffic, traffic_src = load_traffic(args.precision)
+    traffic, traffic_src = load_traffic(precision)
     kernels = {}
     for i, s in enumerate(STAGES):
         if cnt[i] == 0:
@@ -157,30 +152,51 @@ def main():
         kernels[s] = {"ms": round(avg, 4), "bound": bound, "achieved": round(ach, 1), "peak": peak, "unit": unit,
                       "frac": round(ach / peak, 4), "algorithmic_bytes": by, "algorithmic_flop": fl,
                       "traffic": traffic.get(s)}
-    lib_stages = ["proj0", "proj1"] + (["output"] if not f16 else [])
     dom = max(kernels, key=lambda k: kernels[k]["ms"])
     d = kernels[dom]
     line = {
         "metric": "CTC utterances/s (3 s @16 kHz, log-mel 80 -> BiGRU x2 H128 -> greedy CTC), config 5",
         "value": round(value, 1), "unit": "utterances/s", "higher_is_better": True,
-        "audio_seconds_per_s": round(value * args.seconds, 1), "n_gpus": 1,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+        "audio_seconds_per_s": round(value * seconds, 1), "n_gpus": 1,
+        "steps": steps, "warmup": warmup, "ms_per_step": round(el / steps * 1e3, 3),
         "dtype": "f32" if not f16 else "f16 GEMM/MFMA operands, f32 accumulate, f32 gate math and front-end",
         "data": "synthetic (device generator), seeded GRU_CTC_Model weights (the reference ships none)",
         "config": {"workload": "config5: CTC head, 3 s utterances", "batch": B, "vocab": V, "T": T,
-                   "precision": args.precision,
-                   "call": "wk_ctc_features + wk_ctc_forward" if args.separate else "wk_ctc_transcribe"
+                   "precision": precision,
+                   "call": "wk_ctc_features + wk_ctc_forward" if separate else "wk_ctc_transcribe"
                    + (" (z-score folded into the encoder)" if zfold else "")},
         "roofline": {"kernel": dom, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
                      "unit": d["unit"], "frac": d["frac"], "traffic": d["traffic"]},
         "kernels": kernels,
         "stage_sum_ms": round(sum(k["ms"] for k in kernels.values()), 4),
-        "library_stages": {s: "rocBLAS GEMM (Cijk_*)" for s in lib_stages if s in kernels},
     }
     if traffic_src:
         line["traffic_source"] = traffic_src
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--vocab", type=int, default=4000)
+    ap.add_argument("--seconds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cpu-utts", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", default="fp16", choices=["fp32", "fp16"],
+                    help="GEMM operand precision (config 5 names fp16; fp32 is the parity mode)")
+    ap.add_argument("--separate", action="store_true",
+                    help="time wk_ctc_features + wk_ctc_forward instead of the one-call wk_ctc_transcribe")
+    args = ap.parse_args()
+    keep = {}
+    line = run_ctc(args.batch, args.vocab, args.seconds, args.steps, args.warmup, args.precision, args.separate,
+                   keep=keep)
     if not args.no_cpu_baseline:
-        x = torch.from_numpy(audio[:args.cpu_utts].cpu().numpy())
+        import torch
+        from oracle import wk_ctc_oracle as CO
+        m = CO.make_model(args.vocab, seed=0)   # the same seeded weights (wakeword.ctc.random_state_dict)
+        x = torch.from_numpy(keep["audio"][:args.cpu_utts].cpu().numpy())
         with torch.no_grad():
             CO.greedy_decode(m(CO.features(x[:2])))
             c0 = time.perf_counter()
@@ -189,7 +205,8 @@ def main():
         line["cpu_baseline"] = {"value": round(cpu, 2), "unit": "utterances/s", "cores": torch.get_num_threads(),
                                 "host_cpus": len(os.sched_getaffinity(0)), "kind": "port",
                                 "sample": f"{args.cpu_utts} utterances of {args.seconds} s in one batch, torch-CPU "
-                                          f"oracle (oracle/wk_ctc_oracle.py: torch.stft log-mel, nn.GRU, V={V})"}
+                                          f"oracle (oracle/wk_ctc_oracle.py: torch.stft log-mel, nn.GRU, "
+                                          f"V={args.vocab})"}
     print(json.dumps(line), flush=True)
 
 

@@ -568,9 +568,29 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
     int ln = lane;
     asm volatile("" : "+v"(ln));
     const int cl = ln & (NBF - 1), q = ln >> 2;
-    f32x4 h = *reinterpret_cast<const f32x4*>(FCP + cl * 64 + 4 * q);
+    // In the bf16 family the slice sums are scalar fp32 adds, never f32x4
+    // arithmetic (which is v_pk_add_f32): this wave runs beside the K = 32
+    // convolutions of the other CNN waves on its SIMD (the K = 32 rule,
+    // DESIGN 5.1; tests/test_isa_rules.py).  The fp32 build keeps the packed
+    // adds (its MFMAs are K = 4; scalar measured -1 %, profiles/r06b_ab.txt).
+    float h[4];
+    if constexpr (CM == kConvF32) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(FCP + cl * 64 + 4 * q);
 #pragma unroll
-    for (int w = 1; w < 8; ++w) h += *reinterpret_cast<const f32x4*>(FCP + (w * NBF + cl) * 64 + 4 * q);
+      for (int w = 1; w < 8; ++w) v += *reinterpret_cast<const f32x4*>(FCP + (w * NBF + cl) * 64 + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[r] = v[r];
+    } else {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(FCP + cl * 64 + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[r] = v[r];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(FCP + (w * NBF + cl) * 64 + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[r] += u[r];
+      }
+    }
     float acc = 0.0f;
 #pragma unroll
     for (int i2 = 0; i2 < 4; ++i2) acc = __builtin_fmaf(buf_load(rs, 16 * q, 4 * (kPkF2 + i2)), fmaxf(h[i2], 0.0f), acc);

@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -52,11 +53,12 @@ namespace {
 
 using wk::fail;
 
-int g_threads = 0;   // 0 = hardware concurrency
+std::atomic<int> g_threads{0};   // 0 = hardware concurrency (atomic: wkh_set_threads may race a batch call)
 
 int n_threads() {
   const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-  return g_threads > 0 ? g_threads : hw;
+  const int t = g_threads.load(std::memory_order_relaxed);
+  return t > 0 ? t : hw;
 }
 
 // Run f(begin, end) over [0, n) in contiguous chunks on up to n_threads()
@@ -541,7 +543,7 @@ wk_status wkh_esp_mfcc(const float* signal, int64_t batch, int32_t signal_len, i
 }
 
 int32_t wkh_set_threads(int32_t n) {
-  if (n >= 0) g_threads = n;
+  if (n >= 0) g_threads.store(n, std::memory_order_relaxed);
   return n_threads();
 }
 

@@ -44,6 +44,35 @@ def ctc_state_dict_spec(vocab: int, hidden: int = 128, layers: int = 2, n_mels: 
     return spec
 
 
+def random_state_dict(vocab: int, seed: int = 0, hidden: int = 128, layers: int = 2, n_mels: int = 80,
+                      out_scale: float = 4.0) -> Dict[str, np.ndarray]:
+    """Seeded random GRU_CTC_Model weights (the reference ships no trained CTC
+    weights; ctc.py:119-146).  torch's default initialisers, drawn in the
+    module's registration order after torch.manual_seed(seed) -- nn.Linear,
+    nn.LayerNorm, nn.GRU(bidirectional), nn.Linear -- so a torch model built
+    the same way holds the same values.  out_scale multiplies the output
+    layer's weight: 4 gives the greedy path decision margins (a default init is
+    near-uniform over V)."""
+    import torch
+    from torch import nn
+    gen_state = torch.random.get_rng_state()
+    try:
+        torch.manual_seed(seed)
+        enc = nn.Linear(n_mels, hidden)
+        ln = nn.LayerNorm(hidden)
+        gru = nn.GRU(input_size=hidden, hidden_size=hidden, num_layers=layers, batch_first=True,
+                     dropout=0.2 if layers > 1 else 0.0, bidirectional=True)
+        out = nn.Linear(2 * hidden, vocab)
+    finally:
+        torch.random.set_rng_state(gen_state)
+    sd = {"audio_encoder.0.weight": enc.weight, "audio_encoder.0.bias": enc.bias,
+          "audio_encoder.1.weight": ln.weight, "audio_encoder.1.bias": ln.bias}
+    sd.update({f"gru.{k}": v for k, v in gru.state_dict().items()})
+    sd["output_layer.weight"] = out.weight * out_scale
+    sd["output_layer.bias"] = out.bias
+    return {k: v.detach().numpy().astype(np.float32) for k, v in sd.items()}
+
+
 def _as_f32(v) -> np.ndarray:
     if hasattr(v, "detach"):          # torch tensor (any device)
         v = v.detach().cpu().numpy()

@@ -56,7 +56,11 @@ def lib():
     with _lock:
         if _lib is None:
             if not os.path.exists(HOST_LIB_PATH):
-                raise HostError(f"{HOST_LIB_PATH} not found: build it with `python -m wakeword.build`")
+                try:   # built on demand (wakeword.build.build() does not fail on it)
+                    from .build import build_host
+                    build_host()
+                except (RuntimeError, OSError) as e:
+                    raise HostError(f"{HOST_LIB_PATH} not found and could not be built: {e}") from e
             L = C.CDLL(HOST_LIB_PATH, mode=C.RTLD_LOCAL)
             vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
             L.wkh_create.argtypes = [_fp, C.POINTER(vp)]
@@ -144,7 +148,11 @@ def extract_mfcc(signal, signal_len: Optional[int] = None, sampling_rate: int = 
     free_mfcc): (n_frames, n_mfcc) float32, or None where the reference
     returns NULL."""
     x = np.ascontiguousarray(np.asarray(signal, np.float32))
+    if x.ndim != 1:
+        raise ValueError(f"signal must be 1-D, got shape {x.shape}")
     n = int(x.shape[0] if signal_len is None else signal_len)
+    if n > x.shape[0]:   # the C side would read past the array
+        raise ValueError(f"signal_len {n} exceeds the signal's {x.shape[0]} samples")
     L = lib()
     p = L.extract_mfcc(x.ctypes.data_as(_fp), n, sampling_rate, frame_size, hop_size, n_fft, n_filters, n_mfcc)
     if not p:

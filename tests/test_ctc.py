@@ -300,6 +300,21 @@ def test_ctc_state_dict_bound_by_name():
         pack_state_dict(sd, 40)         # vocab disagrees with output_layer
 
 
+def test_random_state_dict_equals_oracle_seeded_model():
+    """wakeword.ctc.random_state_dict (the bench's config-5 weights, no oracle
+    import on the product side) draws the same values as the oracle's seeded
+    GRU_CTC_Model, in its state-dict order, and leaves torch's global RNG as
+    it found it (host-only)."""
+    from wakeword.ctc import ctc_state_dict_spec, random_state_dict
+    before = torch.random.get_rng_state()
+    sd = random_state_dict(53, seed=3)
+    assert torch.equal(before, torch.random.get_rng_state())
+    ref = CO.make_model(53, seed=3).state_dict()
+    assert list(sd) == list(ref) == [k for k, _ in ctc_state_dict_spec(53)]
+    for k in sd:
+        np.testing.assert_array_equal(sd[k], ref[k].numpy())
+
+
 def test_ctc_decode_predictions_text_round_trip():
     """decode_predictions (ctc.py:453-471): argmax, blank drop, repeat collapse,
     idx_to_char with "<unk>" for unmapped ids -- text equals the oracle's token

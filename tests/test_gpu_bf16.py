@@ -114,3 +114,29 @@ def test_fused_repeatable_at_scale(gpu, golden_dir, precision):
         got = m.detect(x).reshape(-1)
         assert int((got != ref).sum()) == 0
     m.check_device_errors()
+
+
+@pytest.mark.parametrize("prec,atol,rtol", [("bf16", BF16_LOGIT_ATOL, 0.02), ("bf16x3", 1e-3, 1e-5)])
+def test_cnn_only_bf16_family_full_size_repeatable(gpu, golden_dir, prec, atol, rtol):
+    """wk_cnn_fused_kernel in the bf16 family at 65,536 clips (config 2's
+    size; four K = 32 waves per SIMD, two CNN roles per workgroup): two
+    launches are bit-identical and every logit is within the precision's
+    tolerance of the fp32 CNN on the same features (the K = 32 rule,
+    DESIGN 5.1 / tests/test_isa_rules.py, checked at run time).  The
+    features are N(0, 1) draws (CMVN'd features are unit-variance per
+    coefficient), so logits run larger than on speech: the bound is
+    atol + rtol |fp32 logit|."""
+    import wakeword
+    torch = gpu
+    g = torch.Generator(device="cuda:0").manual_seed(6)
+    x = torch.randn((65536, 13, 63), generator=g, device="cuda:0", dtype=torch.float32)
+    m = wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"), precision=prec)
+    m32 = wakeword.load_onnx(os.path.join(golden_dir, "xiaoa.onnx"), precision="fp32")
+    a = m(x).reshape(-1)
+    b = m(x).reshape(-1)
+    ref = m32(x).reshape(-1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b), int((a != b).sum())
+    excess = (a - ref).abs() - (atol + rtol * ref.abs())
+    assert float(excess.max()) <= 0.0, float((a - ref).abs().max())

@@ -162,6 +162,11 @@ def test_extract_mfcc_refusals(host):
     assert host.extract_mfcc(x, 16000, 16000, 0, 160, 512, 40, 13) is None
     L = host.lib()
     assert not L.extract_mfcc(None, 16000, 16000, 320, 256, 512, 40, 13)
+    # the Python wrapper refuses a signal_len past the array (the C side would over-read) and non-1-D input
+    with pytest.raises(ValueError):
+        host.extract_mfcc(x[:1000], 16000)
+    with pytest.raises(ValueError):
+        host.extract_mfcc(x.reshape(2, -1))
 
 
 @pytest.mark.parametrize("cfg", [(16000, 320, 512, 40, 13), (8000, 200, 256, 26, 12), (16000, 512, 512, 64, 13)])

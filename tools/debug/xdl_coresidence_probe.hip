@@ -103,6 +103,24 @@ __device__ __forceinline__ f32x2 p_mul_negi_pk(f32x2 v) {
   asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(v), "v"(c));
   return r;
 }
+// The quarter turn -i v as the compiler builds it in sub 5 -- two v_mov_b32
+// into the halves of a register pair, then a packed op reading the pair --
+// written out in asm on a fixed pair (v80:v81) so the spacing is exact:
+// NOP = false back to back (the bisected form), true with s_nop 7 (8 wait
+// states) between the pair's writes and the packed read.  The round-6
+// wait-state experiment (DESIGN.md 5.1, K = 32 rule).
+template <bool NOP>
+__device__ __forceinline__ f32x2 p_mul_negi_movpair(f32x2 v) {
+  f32x2 r;
+  const f32x2 c = {1.0f, -1.0f};
+  if (NOP)
+    asm volatile("v_mov_b32 v80, %1\n\tv_mov_b32 v81, %2\n\ts_nop 7\n\tv_pk_mul_f32 %0, v[80:81], %3"
+                 : "=v"(r) : "v"(v.y), "v"(v.x), "v"(c) : "v80", "v81");
+  else
+    asm volatile("v_mov_b32 v80, %1\n\tv_mov_b32 v81, %2\n\tv_pk_mul_f32 %0, v[80:81], %3"
+                 : "=v"(r) : "v"(v.y), "v"(v.x), "v"(c) : "v80", "v81");
+  return r;
+}
 template <int KA>
 __device__ __forceinline__ void p_rowgroup(f32x2 (&a)[16]) {
 #pragma unroll
@@ -216,7 +234,9 @@ __global__ __launch_bounds__(kThreads) void probe_kernel(int iters, int VAR, con
                                   // 3 one DFT4 pass; 4 the DFT4 pass of rows only (no swapped operands: a0/a2 sums);
                                   // 5 twiddles + the row pass; 6 the column pass + twiddles;
                                   // 7-9 row group ka = sub - 6 alone (twiddles + DFT4);
-                                  // 10 sub 5 with the quarter turn as one packed op
+                                  // 10 sub 5 with the quarter turn as one packed op;
+                                  // 11 / 12 sub 5 with the quarter turn as an explicit v_mov_b32 pair
+                                  // + packed read, with (11) / without (12) 8 wait states between them
       for (int it = 0; it < iters; ++it) {
         if (sub == 0) {
           p_dft16(d);
@@ -251,6 +271,16 @@ __global__ __launch_bounds__(kThreads) void probe_kernel(int iters, int VAR, con
               d[4 * ka + nb] = (nb * ka == 4) ? p_mul_negi_pk(d[4 * ka + nb]) : p_twid(d[4 * ka + nb], nb * ka);
 #pragma unroll
           for (int ka = 0; ka < 4; ++ka) p_dft4(d[4 * ka], d[4 * ka + 1], d[4 * ka + 2], d[4 * ka + 3]);
+        } else if (sub == 11 || sub == 12) {   // sub 5, the quarter turn as an explicit v_mov_b32 pair (+ s_nop 7 in 11)
+#pragma unroll
+          for (int ka = 1; ka < 4; ++ka)
+#pragma unroll
+            for (int nb = 1; nb < 4; ++nb)
+              d[4 * ka + nb] = (nb * ka != 4)   ? p_twid(d[4 * ka + nb], nb * ka)
+                               : sub == 11 ? p_mul_negi_movpair<true>(d[4 * ka + nb])
+                                           : p_mul_negi_movpair<false>(d[4 * ka + nb]);
+#pragma unroll
+          for (int ka = 0; ka < 4; ++ka) p_dft4(d[4 * ka], d[4 * ka + 1], d[4 * ka + 2], d[4 * ka + 3]);
         } else if (sub == 7) {   // one row group ka = sub - 6: its twiddles, then its DFT4
           p_rowgroup<1>(d);
         } else if (sub == 8) {
@@ -270,7 +300,7 @@ __global__ __launch_bounds__(kThreads) void probe_kernel(int iters, int VAR, con
             d[12 + nb] = t1 - t3;
           }
         }
-        const float sc = sub == 2 ? 1.0f : sub >= 3 ? 0.5f : 0.25f;   // (10 too)   // (5, 6: one pass, x 1/2)   // keeps the norm
+        const float sc = sub == 2 ? 1.0f : sub >= 3 ? 0.5f : 0.25f;   // (10-12 too)   // (5, 6: one pass, x 1/2)   // keeps the norm
 #pragma unroll
         for (int q = 0; q < 16; ++q) d[q] *= f32x2{sc, sc};
       }
