@@ -34,6 +34,8 @@ struct wk_handle {
   int unfused;           // WAKEWORD_UNFUSED=1: front-end + CNN as two kernels (A/B testing)
   int fused_exp;         // WAKEWORD_FUSED_EXP, -DWK_DIAG builds only: role-isolation timing
                          // experiments (wrong logits); always 0 in the shipped library
+  int fe_wg_per_cu = 2;  // standalone front-end workgroups per CU (WAKEWORD_FE_WG_PER_CU, -DWK_DIAG builds
+                         // only: the occupancy experiment of DESIGN 5.1); 2 in the shipped library
 };
 
 namespace wk {
@@ -106,6 +108,8 @@ wk_status wk_create(const wk_config* cfg, const float* host_weights, wk_handle**
 #ifdef WK_DIAG
     const char* fx = getenv("WAKEWORD_FUSED_EXP");
     h->fused_exp = fx ? atoi(fx) : 0;
+    const char* fw = getenv("WAKEWORD_FE_WG_PER_CU");
+    if (fw && (atoi(fw) == 1 || atoi(fw) == 2)) h->fe_wg_per_cu = atoi(fw);
 #endif
   }
   wk_status st = on_device(cfg->device, [&]() -> wk_status {
@@ -222,7 +226,7 @@ wk_status wk_mfcc(wk_handle* h, const void* d_audio, int32_t dtype, int64_t batc
   if (batch > 0 && !d_feats) return invalid("wk_mfcc: null feats");
   return on_device(h->cfg.device, [&]() -> wk_status {
     hipError_t e = wk::launch_frontend(mode_b, dtype == WK_DTYPE_I16, d_audio, batch, win_len, clip_stride, d_feats,
-                                       h->cfg.esp_dsp_packing, h->cfg.cmvn, 2 * h->n_cu, 0.97f,
+                                       h->cfg.esp_dsp_packing, h->cfg.cmvn, h->fe_wg_per_cu * h->n_cu, 0.97f,
                                        (hipStream_t)stream);
     return e == hipSuccess ? WK_OK : hip_fail(e, "frontend launch");
   });

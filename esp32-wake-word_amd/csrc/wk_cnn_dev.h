@@ -16,17 +16,6 @@ namespace wk {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#ifdef WK_DIAG_PROW
-// Diagnostic builds only (the K = 32 question): every epilogue
-// store's element index is checked against its image (4 clips x rows x pitch)
-// or the pooled-feature array; an index outside sets this word
-// (wk_debug_epi_bad in wk_fused.hip reads it).
-static __device__ unsigned g_epi_bad;
-#define WK_EPI_GUARD(idx, lim) do { if ((unsigned)(idx) >= (unsigned)(lim)) g_epi_bad = 1u; } while (0)
-#else
-#define WK_EPI_GUARD(idx, lim) do {} while (0)
-#endif
-
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -56,7 +45,6 @@ __device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g,
     s += dpp<0x141>(s);
     s += dpp<0x140>(s);
     if (tt == 0) {
-      WK_EPI_GUARD((co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip, 128 * GSTRIDE);
       g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s * (1.0f / 7.0f);
     }
   }
@@ -64,67 +52,32 @@ __device__ __forceinline__ void epi_gap(const f32x4& acc, float* __restrict__ g,
 
 // ---- bf16 convolutions (WK_PREC_BF16 / BF16X3) -----------------------------
 // Fragments hold 8 bf16 per lane (K = 32 per step): one 16-byte LDS read per
-// B fragment and one 16-byte load per A fragment.  A step is issued as two
-// CDNA3-era v_mfma_f32_16x16x16_bf16 (elements 0-3, then 4-7 of each lane).
-// gfx950's single-instruction K=32 form (v_mfma_f32_16x16x32_bf16) is the
-// same work in the same ~16 cycles as ONE K=16 instruction, but with it the
-// fused kernel's front-end log-mel images changed run to run (round 3,
-// DESIGN.md 5.1): the cause was not found, so the form is not used.  What
-// bounds the K=16 pair's exposure to the same unknown: the CNN carve is
-// disjoint from the front-end's power rows and log-mel buffers
-// (static_asserts in wk_fused.hip), and four full-size launches per precision
-// are compared bit for bit (tests/test_gpu_bf16.py::test_fused_repeatable_at_scale).
+// B fragment and one 16-byte load per A fragment.  Product builds issue a step
+// as gfx950's v_mfma_f32_16x16x32_bf16.  The K = 32 rule: no
+// kernel that issues it may issue packed-fp32 VALU (v_pk_*_f32), which was seen
+// corrupted in lanes 48-63 beside it on the same SIMD.  The bf16-family fused
+// unit (wk_fused_xdl.hip) therefore runs its front-end in scalar fp32, and
+// tests/test_isa_rules.py checks every kernel of the library.  Diagnostic
+// one-unit builds (WK_FUSED_ONE_TU: packed front-end in every precision) issue
+// the step as two CDNA3-era v_mfma_f32_16x16x16_bf16 instead.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s8 __attribute__((ext_vector_type(8)));   // one lane's A or B fragment: 8 bf16 bit patterns
 
-#if defined(WK_MFMA_K32) && !defined(WK_ALLOW_K32_DIAG)
-#error "WK_MFMA_K32 corrupts the fused kernel's front-end (DESIGN.md 5.1); diagnostic builds add -DWK_ALLOW_K32_DIAG"
-#endif
-// Product (split) builds use the K = 32 form: the bf16-family fused unit's
-// front-end is scalar fp32, and the standalone CNN has none (k32_layer).
-// -DWK_XDL_K32_OFF keeps the K = 16 pair for A/B.
-#if !defined(WK_XDL_K32_OFF) && !defined(WK_XDL_K32)
-#define WK_XDL_K32 1
-#endif
-#ifndef WK_K32_MASK
-#define WK_K32_MASK 7   // diagnostic K = 32 builds: which conv layers use it (bit 0 conv1, 1 conv2, 2 conv3)
-#endif
-// K32 is true only in diagnostic builds (tools/debug/xdl_hazard_scan.py, k32_repeat.py).
 template <bool K32>
 __device__ __forceinline__ f32x4 mfma_bf16(s8 a, s8 b, f32x4 c) {
-  if constexpr (K32) {
-#ifdef WK_K32_F16    // the f16 K = 32 form on the same bit patterns (logits wrong; the features are the probe)
-    typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
-#else
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
-#endif
-#ifdef WK_K32_PAD   // 16 wait states after every K = 32 MFMA, nothing scheduled across them
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-    return c;
-  }
+  if constexpr (K32)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                   0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 0, 1, 2, 3),
                                                 __builtin_shufflevector(b, b, 0, 1, 2, 3), c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_shufflevector(a, a, 4, 5, 6, 7),
                                                    __builtin_shufflevector(b, b, 4, 5, 6, 7), c, 0, 0, 0);
 }
-// the conv layer of a CINP (16: conv1, 32: conv2, 64: conv3) uses the K = 32 form
+// Whether a conv layer (CINP 16: conv1, 32: conv2, 64: conv3) uses the K = 32
+// form: every layer in product builds, none in diagnostic one-unit builds.
 template <int CINP>
 constexpr bool k32_layer() {
-#if defined(WK_MFMA_K32)
-  return (WK_K32_MASK >> (CINP == 16 ? 0 : CINP == 32 ? 1 : 2)) & 1;
-#elif defined(WK_XDL_K32) && !WK_FUSED_ONE_TU
-  // Split product build: the bf16 convolutions run in the bf16-family fused
-  // unit, whose front-end has no packed fp32 (beside which the K = 32 form is
-  // exact), and in the standalone CNN kernel, which has no
-  // front-end; both use it, so the two accumulate alike.
-  return true;
-#else
-  return false;
-#endif
+  return !WK_FUSED_ONE_TU;
 }
 
 __device__ __forceinline__ uint32_t bf16_bits(float x) {   // round to nearest even
@@ -182,7 +135,6 @@ __device__ __forceinline__ void epi_pool_bf(const f32x4& acc, uint16_t* __restri
     uint2 pkd;
     pkd.x = bf16_bits(v[0]) | (bf16_bits(v[1]) << 16);
     pkd.y = bf16_bits(v[2]) | (bf16_bits(v[3]) << 16);
-    WK_EPI_GUARD((clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4) + 3, 4 * TP_N * CIP_N);
     *reinterpret_cast<uint2*>(next + (clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4)) = pkd;
   }
 }
@@ -231,7 +183,6 @@ __device__ __forceinline__ void epi_pool_bf3(const f32x4& acc, uint16_t* __restr
     l[r] = bf16_bits(v - __uint_as_float(h[r] << 16));
   }
   if (!(lane & 1) && tp < TN) {
-    WK_EPI_GUARD((clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4) + LO + 3, 4 * TP_N * CIP_N);
     uint16_t* p = next + (clip * TP_N + 1 + tp) * CIP_N + co0 + 4 * (lane >> 4);
     *reinterpret_cast<uint2*>(p) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
     *reinterpret_cast<uint2*>(p + LO) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
@@ -296,7 +247,6 @@ __device__ __forceinline__ void epi_wino_pool(const f32x4 (&m)[4], float* __rest
     v[r] = fmaxf(fmaxf(y0, y1), 0.0f);
   }
   if (p < TN) {
-    WK_EPI_GUARD((clip * TP_N + 1 + p) * CIP_N + co0 + 4 * (lane >> 4) + 3, 4 * TP_N * CIP_N);
     *reinterpret_cast<float4*>(next + (clip * TP_N + 1 + p) * CIP_N + co0 + 4 * (lane >> 4)) =
         make_float4(v[0], v[1], v[2], v[3]);
   }
@@ -316,7 +266,6 @@ __device__ __forceinline__ void epi_wino_gap(const f32x4 (&m)[4], float* __restr
     s += dpp<0x4E>(s);
     s += dpp<0x141>(s);
     if (p == 0) {
-      WK_EPI_GUARD((co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip, 128 * GSTRIDE);
       g[(co0 + 4 * (lane >> 4) + r) * GSTRIDE + clip] = s * (1.0f / 7.0f);
     }
   }

@@ -18,8 +18,7 @@ constexpr int kFeBlock = 512;        // 8 waves per front-end workgroup
 // Diagnostic builds (and -DWK_FE_PACKED_ALL, the A/B baseline) compile the
 // whole fused kernel in one translation unit (wk_fused.hip), with the packed
 // front-end in every precision.
-#if defined(WK_DIAG) || defined(WK_DIAG_PROW) || defined(WK_DIAG_FEDUMP) || defined(WK_DIAG_SIMD_SPLIT) || \
-    defined(WK_DIAG_K32_SPIN) || defined(WK_MFMA_K32) || defined(WK_FE_PACKED_ALL)
+#if defined(WK_DIAG) || defined(WK_FE_PACKED_ALL)
 #define WK_FUSED_ONE_TU 1
 #else
 #define WK_FUSED_ONE_TU 0
@@ -93,20 +92,7 @@ __device__ __forceinline__ f2 w16(int e) {
   }
 }
 
-#if defined(WK_QTURN_PK) && !(defined(WK_FE_SCALAR) && defined(WK_FUSED_TU))
-// s * swap(v) as ONE v_pk_mul_f32 (the swap in op_sel, the signs in an SGPR
-// pair).  Left to itself the compiler builds swp(v) with two v_mov_b32 into
-// the halves of a register pair; with a K = 32 MFMA in flight on the same
-// SIMD, packed ops reading such a pair came out wrong in lanes 48-63
-// (the K = 32 question; tools/debug/xdl_coresidence_probe.hip).
-__device__ __forceinline__ f2 swap_mul(f2 v, f2 s) {
-  f2 r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(v), "s"(s));
-  return r;
-}
-#else
 __device__ __forceinline__ f2 swap_mul(f2 v, f2 s) { return swp(v) * s; }
-#endif
 // v * W16^e with the quarter turns folded (e is a constant after unrolling).
 __device__ __forceinline__ f2 twid16(f2 v, int e) {
   switch (e & 15) {

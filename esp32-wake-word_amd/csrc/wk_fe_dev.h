@@ -235,34 +235,13 @@ __device__ __forceinline__ void fe_stage0(const Raw<T>& raw, int base, int n, in
 // 8 ds_read2_b64 (the re / im two-pass transpose was 16 write2 + 32 reads).
 // The second DFT16 then sees its inputs rotated by 8 in lanes kc >= 8, which
 // multiplies Z[kc + 16 k2] by (-1)^k2 there; fe_split_tw absorbs the sign.
-// Diagnostic (-DWK_DIAG_FEDUMP, the K = 32 question of DESIGN.md 5.1): a
-// per-lane dump pointer; the lane's 16 complex registers are stored at four
-// points (k = 0 the stage-0 output, 1 after the first DFT16, 2 after the LDS
-// transpose, 3 after the second DFT16) as [4][16 lanes][32] floats.
-#ifdef WK_DIAG_FEDUMP
-#define WK_FD_PARAM , float* fdump = nullptr
-#define WK_FE_DUMP(k, arr)                                  \
-  do {                                                      \
-    if (fdump) {                                            \
-      _Pragma("unroll") for (int q_ = 0; q_ < 16; ++q_) {   \
-        fdump[(k) * 512 + j * 32 + 2 * q_] = (arr)[q_].x;    \
-        fdump[(k) * 512 + j * 32 + 2 * q_ + 1] = (arr)[q_].y; \
-      }                                                     \
-    }                                                       \
-  } while (0)
-#else
-#define WK_FD_PARAM
-#define WK_FE_DUMP(k, arr) do {} while (0)
-#endif
 template <bool MODE_B, typename PF, typename TWS>
 __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ row, float* __restrict__ xs,
                                         const FeTables& tb, f2 w0, const TWS& tws, int esp_pack,
-                                        const PF& pf WK_SP_PARAM WK_FD_PARAM) {
-  WK_FE_DUMP(0, a);
+                                        const PF& pf WK_SP_PARAM) {
   pf(0);
   dft16(a);  // slot s: A[s ^ (j & 8)] at a[dft16_out(s)]
   WK_FE_HIT(2);
-  WK_FE_DUMP(1, a);
 
   // twiddle W256^(n2 k1), n2 = j, k1 = s ^ (j & 8); each half is twiddled
   // just before it is written (fewer live registers)
@@ -291,13 +270,11 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
   for (int s = 8; s < 16; ++s) c[s] = x2[(j ^ 8) + 17 * (s - 8)];
   wave_lds_sync();
   WK_FE_HIT(4);
-  WK_FE_DUMP(2, c);
 
   pf(2);
   dft16(c);  // +-Z[j + 16*k2] at c[dft16_out(k2)]
   pf(3);
   WK_FE_HIT(5);
-  WK_FE_DUMP(3, c);
 
   // Real-FFT split, k = j + 16*k2 (k2 = 0..7), with the partner Z[256 - k]:
   //   S = Z[k] + conj Z[256-k],  D = Z[k] - conj Z[256-k],  bb = W512^k D,
@@ -343,24 +320,10 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
       // bound_ctrl off: lane 0 has no source and keeps `old` = its own
       // partner register -- no lane select.
       f2 zq;
-#ifdef WK_SPLIT_BPERM   // diagnostic (the K = 32 question): the partner by ds_bpermute, no DPP
-      {
-        const int src = ((int)__lane_id() & ~15) | ((16 - j) & 15);
-        const float px = __shfl(sv.x, src, 64), py = __shfl(sv.y, src, 64);
-        zq.x = j == 0 ? own.x : px;
-        zq.y = j == 0 ? own.y : py;
-      }
-#else
-#ifdef WK_SPLIT_DPP_PAD   // diagnostic: 5 extra wait states ahead of the partner's DPP moves
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_nop 4" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-#endif
       zq.x = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.x), __float_as_int(dpp<0x140>(sv.x)),
                                                         0x111, 0xF, 0xF, false));
       zq.y = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), __float_as_int(dpp<0x140>(sv.y)),
                                                         0x111, 0xF, 0xF, false));
-#endif
       S[t] = fma2(zq, f2{1.0f, -1.0f}, zk);
       D[t] = fma2(zq, f2{-1.0f, 1.0f}, zk);
     }

@@ -51,27 +51,6 @@ __device__ unsigned long long g_wk_stamps[16][16];
 #define WK_SP_ARG
 #endif
 
-#ifdef WK_DIAG_PROW
-// Diagnostic builds only (-DWK_DIAG_PROW, tools/debug/prow_probe.py; the K = 32
-// question of DESIGN.md 5.1): the power rows of each workgroup's first
-// kProwClips clips, three snapshots [3][grid * kProwClips][64][257]: A = what
-// each front-end lane wrote (read back right after its round), B = the rows
-// after the clip's role barrier, just before the mel reads them, C = the same
-// rows after the mel.
-__device__ float* g_prow_dbg;
-// ... and the same clips' log-mel images [2][grid * kProwClips][40][64]: D = as
-// the front-end's mel left them, E = as the CNN wave's DCT is about to read them.
-__device__ float* g_lmel_dbg;
-#ifndef WK_PROW_CLIPS
-#define WK_PROW_CLIPS 32
-#endif
-constexpr int kProwClips = WK_PROW_CLIPS;
-#endif
-#ifdef WK_DIAG_FEDUMP
-// ... and the front-end registers of the same clips' frames at four points of
-// fe_rest ([grid * kProwClips][64 frames][4][16 lanes][32]; wk_fe_dev.h).
-__device__ float* g_fe_dump;
-#endif
 
 
 constexpr int NBF = 4;               // clips per CNN batch
@@ -332,43 +311,10 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       };
       WK_STAMP(1);
       float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
-#ifdef WK_DIAG_FEDUMP
-      float* fd = (i < kProwClips && fl < kNFramesB && g_fe_dump)
-                      ? g_fe_dump + ((size_t)(blockIdx.x * kProwClips + i) * 64 + fl) * 2048
-                      : nullptr;
-      fe_rest<true>(a, j, row, row + (fl & 1), tb, w0, tws, 0, pf_part WK_SP_ARG, fd);
-#else
       fe_rest<true>(a, j, row, row + (fl & 1), tb, w0, tws, 0, pf_part WK_SP_ARG);
-#endif
-#ifdef WK_DIAG_PROW
-      if (i < kProwClips && fl < kNFramesB && g_prow_dbg) {   // snapshot A: this lane's bins as it wrote them
-        float* dA = g_prow_dbg + ((size_t)(blockIdx.x * kProwClips + i) * 64 + fl) * 257;
-        for (int k2 = 0; k2 < 8; ++k2) {
-          dA[j + 16 * k2] = row[j + 16 * k2];
-          dA[256 - j - 16 * k2] = row[256 - j - 16 * k2];
-        }
-        if (j == 0) dA[128] = row[128];
-      }
-#endif
     }
     role_sync<kPrioFe>(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
     WK_STAMP(7);
-#ifdef WK_DIAG_PROW
-    auto prow_snap = [&](int k) {   // snapshots B (k = 1) and C (k = 2): wave w copies frames w, w + 8, ...
-      if (i >= kProwClips || !g_prow_dbg) return;
-      float* d = g_prow_dbg + (size_t)k * gridDim.x * kProwClips * 64 * 257;
-      for (int f = wave; f < kNFramesB; f += 8)
-        for (int b = lane; b < 257; b += 64) d[((size_t)(blockIdx.x * kProwClips + i) * 64 + f) * 257 + b] = P[f * kPRow + b];
-    };
-    prow_snap(1);
-    if (i >= 1 && i - 1 < kProwClips && g_lmel_dbg) {
-      // snapshot D of clip i - 1: its log-mel image as the front-end's mel left it (complete: every wave has
-      // passed this clip's barrier since; the buffer is next written by clip i + 1's mel), wave w rows w, w + 8, ...
-      const float* lb = ((i - 1) & 1 ? L1 : L);
-      float* d = g_lmel_dbg + (size_t)(blockIdx.x * kProwClips + i - 1) * 40 * 64;
-      for (int m = wave; m < 40; m += 8) d[m * 64 + lane] = lb[m * WK_LSTRIDE + lane];
-    }
-#endif
     if (i >= 2 && !(diag & 1)) spin_until_all8<kPrioFe>(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
     WK_STAMP(10);
     {
@@ -381,9 +327,6 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       mel_dispatch<true>(wave, smem + prow, (i & 1 ? L1 : L) + lane);
     }
     WK_STAMP(8);
-#ifdef WK_DIAG_PROW
-    prow_snap(2);
-#endif
     signal_add(ctrl, kCtrlLReady, lane);
     // Split barrier: arrive now, wait before this wave next writes a power
     // row (round 0 of clip i+1), after its stage 0 and prefetch.
@@ -813,13 +756,6 @@ struct LogmelSrc {
     if (!(diag & 2)) spin_until<0>(ctrl, kCtrlLReady, 8u * (unsigned)(i + 1));
   }
   __device__ __forceinline__ void load(int64_t i, int slot) const {
-#ifdef WK_DIAG_PROW
-    if (i < kProwClips && g_lmel_dbg) {   // snapshot E: the whole image as this CNN wave is about to read it
-      const float* lb = smem + (i & 1 ? kL1Off : kLOff);
-      float* d = g_lmel_dbg + ((size_t)gridDim.x * kProwClips + clip_base * kProwClips + i) * 40 * 64;
-      for (int e = lane; e < 40 * 64; e += 64) d[e] = lb[(e >> 6) * WK_LSTRIDE + (e & 63)];
-    }
-#endif
     float* fo = FEATS ? feats_out + (clip_base + clip_step * i) * (13 * kNFramesB) : nullptr;
     dct_cmvn_clip<CM>(smem + (i & 1 ? kL1Off : kLOff), slot, smem + kF0Off,
                       reinterpret_cast<uint16_t*>(smem + kB0Off), reinterpret_cast<uint16_t*>(smem + kX0Off), fo,
@@ -853,42 +789,9 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
 #endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-#ifdef WK_DIAG_SIMD_SPLIT
-  // Diagnostic (K = 32 question): the roles by hardware SIMD --
-  // front-end waves on SIMDs 0-1, CNN waves on SIMDs 2-3 -- instead of by wave
-  // index (which puts two of each role on every SIMD).  HW_ID bits 5:4 are the
-  // SIMD; a per-SIMD LDS counter gives the slot.  A SIMD with more than four
-  // waves leaves the default mapping (and is reported in err bit 8).
-  __shared__ unsigned simd_slot[4];
-  if (tid < 4) simd_slot[tid] = 0;
-  __syncthreads();
-  int wave;
-  {
-    const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // hwreg(HW_REG_HW_ID, 0, 32)
-    const int simd = (int)((hw >> 4) & 3u);
-    unsigned slot = 0;
-    if (lane == 0) slot = atomicAdd(&simd_slot[simd], 1u);
-    slot = __builtin_amdgcn_readfirstlane(slot);
-    wave = (simd >> 1) * 8 + (simd & 1) * 4 + (int)slot;
-    if (slot > 3u) {
-      wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-      if (lane == 0) atomicOr(err, 256u);
-    }
-    wave = __builtin_amdgcn_readfirstlane(wave);
-  }
-#else
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-#endif
   fe_init_tables<true, true>(smem, tid, kFusedBlock);
   for (int i = tid; i < kFusedLds - kGOff; i += kFusedBlock) smem[kGOff + i] = 0.0f;  // ctrl, guards, pads
-#ifdef WK_DIAG_K32_SPIN
-  // Diagnostic (K = 32 question; -DWK_DIAG builds, front-end-only
-  // mode): the CNN waves run a bare MFMA stream on register operands --
-  // WK_DIAG_K32_SPIN=1 the K = 32 bf16 form, 0 the K = 16 pair -- for as long
-  // as the front-end role runs, with no LDS traffic of their own.
-  __shared__ unsigned fe_done;
-  if (tid == 0) fe_done = 0;
-#endif
   __syncthreads();
   const int64_t n_mine = batch > (int64_t)blockIdx.x ? (batch - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   // The front-end role is the critical path: static issue priority over the
@@ -897,28 +800,7 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
   if (wave < 8) __builtin_amdgcn_s_setprio(kPrioFe);
   if (wave < 8) {
     if (!(diag & 2)) fe_role<T>(smem, audio, n_mine, clip_stride, feats_out, wave, lane, diag);
-#ifdef WK_DIAG_K32_SPIN
-    if (lane == 0) atomicAdd(&fe_done, 1u);
-#endif
   } else {
-#ifdef WK_DIAG_K32_SPIN
-    if (diag & 1) {
-      f32x4 acc[4] = {};
-      s8 a, b;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        a[q] = (short)(0x3c00 + ((lane + q) & 7));
-        b[q] = (short)(0x3c00 + ((3 * lane + q) & 7));
-      }
-      for (int n = 0; n < (1 << 22); n += 16) {   // bounded: ~4 M MFMAs at most
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j & 3] = mfma_bf16<WK_DIAG_K32_SPIN != 0>(a, b, acc[j & 3]);
-        if (__builtin_amdgcn_readfirstlane(*(volatile unsigned*)&fe_done) >= 8u) break;
-      }
-      if (feats_out) reinterpret_cast<f32x4*>(feats_out)[(size_t)blockIdx.x * 512 + (wave - 8) * 64 + lane] =
-          acc[0] + acc[1] + acc[2] + acc[3];   // (keeps the MFMAs; the feature output is not read in this mode)
-    }
-#endif
     if (!(diag & 1)) {
       LogmelSrc<CM, FEATS> src = {smem, reinterpret_cast<unsigned*>(smem + kCtrlOff), feats_out, (int64_t)blockIdx.x,
                                   (int64_t)gridDim.x, 0, 0, diag};
@@ -1004,26 +886,6 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_cnn_fused_kernel(const floa
 }  // namespace
 
 #ifndef WK_FUSED_XDL_TU
-#ifdef WK_DIAG_FEDUMP
-extern "C" int wk_debug_fe_buffer(void* d) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_fe_dump), &d, sizeof(d)) != hipSuccess;
-}
-#endif
-#ifdef WK_DIAG_PROW
-extern "C" int wk_debug_prow_buffer(void* d) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_prow_dbg), &d, sizeof(d)) != hipSuccess;
-}
-extern "C" int wk_debug_lmel_buffer(void* d) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_lmel_dbg), &d, sizeof(d)) != hipSuccess;
-}
-// Reads (and with reset clears) the epilogue bounds-check word of wk_cnn_dev.h.
-extern "C" int wk_debug_epi_bad(unsigned* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_epi_bad), sizeof(unsigned)) != hipSuccess) return 1;
-  const unsigned zero = 0;
-  return reset && hipMemcpyToSymbol(HIP_SYMBOL(g_epi_bad), &zero, sizeof(zero)) != hipSuccess;
-}
-#endif
-
 #ifdef WK_DIAG
 extern "C" int wk_debug_stamps(unsigned long long* host_out, int reset) {
   if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wk_stamps), sizeof(g_wk_stamps)) != hipSuccess) return 1;
