@@ -30,10 +30,12 @@ cd "$R"
 timeout -k 10 300 python3 bench.py $BARGS > "$OUT/bench.log" 2> "$OUT/bench.err"
 echo "bench: $(tail -1 $OUT/bench.log | cut -c1-200)"
 cd /tmp && export TMPDIR=/tmp
+# 40 timed steps so the 2 warm-up launches weigh little in the kernel's mean; the
+# profiled bench line (prof.log) carries the same command's own HIP-event launch time
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 "$R/bench.py" --no-cpu-baseline $BARGS > "$OUT/prof.log" 2>&1
+  python3 "$R/bench.py" --no-cpu-baseline --no-extras --steps 40 --warmup 2 $BARGS > "$OUT/prof.log" 2>&1
 cd "$R"
-timeout -k 10 900 bash tools/profile_pmc.sh "$OUT/pmc" --steps 2 --warmup 1 --no-cpu-baseline $BARGS > "$OUT/pmc.log" 2>&1
+timeout -k 10 900 bash tools/profile_pmc.sh "$OUT/pmc" --steps 2 --warmup 1 --no-cpu-baseline --no-extras $BARGS > "$OUT/pmc.log" 2>&1
 python3 tools/pmc_summary.py "$OUT/pmc" --json "$OUT/${TAG}_pmc.json" > "$OUT/pmc_summary.txt"
 case "$BARGS" in *bf16x3*) BF=2; TF=hbm_traffic_bf16x3.json ;; *bf16*) BF=1; TF=hbm_traffic_bf16.json ;; *) BF=0; TF=hbm_traffic.json ;; esac
 python3 - "$OUT/${TAG}_pmc.json" "$OUT/$TF" "$TAG" "$BF" <<'PY'
