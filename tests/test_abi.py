@@ -93,3 +93,14 @@ def test_every_export_has_a_ctypes_prototype(L):
     for name in _lib.EXPORTS:
         if name not in no_args:
             assert getattr(L, name).argtypes is not None, name
+
+
+def test_product_links_only_the_hip_runtime():
+    """Every kernel is hand-written: the library needs the HIP runtime and the
+    C/C++ runtime, no vendor math library (rocBLAS, hipBLAS(Lt), MIOpen, ...)."""
+    from wakeword import _lib
+    out = subprocess.run(["readelf", "-d", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    needed = re.findall(r"\(NEEDED\)\s+Shared library: \[([^\]]+)\]", out)
+    assert any(n.startswith("libamdhip64") for n in needed), needed
+    banned = ("rocblas", "hipblas", "miopen", "rocfft", "hipfft", "rccl", "rocsparse", "torch")
+    assert not [n for n in needed if any(b in n.lower() for b in banned)], needed
