@@ -576,8 +576,14 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
     role_sync<0>(ctrl, kCtrlCnnBar, gen, lane);   // conv1 image complete (and the previous batch's partials)
     if (b > 0) fc2(b - 1);
 
+    // Clips of this batch that exist (wave-uniform): a short last batch -- and
+    // the one-window launches of the streaming path -- skip the conv passes
+    // that cover only absent clips, which shortens each wave's MFMA chain
+    // (single-window latency).  Full batches run every pass.
+    const int nv = n_mine - b * NBF < NBF ? (int)(n_mine - b * NBF) : NBF;
+
     // conv1: co tile (cw&1), clip (cw>>1), 4 t-tiles.
-    {
+    if ((cw >> 1) < nv) {
       const int co0 = 16 * (cw & 1), cl = cw >> 1;
       const int bo = (cl * I0_TP + li) * I0_CIP;   // this lane's t row in the bf16 [clip][t][ci] image
 #pragma unroll 1
@@ -615,6 +621,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
+        if (cl >= nv) break;
         const int bb = (cl * I1_TP + li) * I1_CIP;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
         conv_pair_bf<3, 32, I1_CIP>(B1, w2b, bb, bb + 16 * I1_CIP, lk, acc_a, acc_b);
@@ -631,6 +638,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
+        if (cl >= nv) break;
         const int bb = (cl * I1_TP + li) * X1_CIP;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
         conv_pair_bf3<3, 32, X1_CIP>(X1, w2b, w2l, bb, bb + 16 * X1_CIP, lk, acc_a, acc_b);
@@ -645,6 +653,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int cl = 2 * (cw >> 2) + p;
+        if (cl >= nv) break;
         f32x4 m[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
         conv_wino_v<2, F1_CIP, 1>(F1, w2, (cl * I1_TP + 2 * li) * F1_CIP + 4 * lk, m);
         epi_wino_pool<F2_CIP, I2_TP, 15>(m, F2, co0, cl, 0, lane);
@@ -662,6 +671,7 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const int ca = 2 * p, cb = 2 * p + 1;
+        if (ca >= nv) break;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
         if constexpr (BF) {
           conv_pair_bf<6, 64, I2_CIP, 3>(B2, w3b, bo + ca * I2_TP * I2_CIP, bo + cb * I2_TP * I2_CIP, lk, acc_a,
