@@ -54,6 +54,13 @@ __device__ unsigned long long g_wk_stamps[16][16];
 
 
 constexpr int NBF = 4;               // clips per CNN batch
+#ifndef WK_FE_WAVES
+#define WK_FE_WAVES 8
+#endif
+#if WK_FE_WAVES != 8 && !defined(WK_DIAG)
+#error "WK_FE_WAVES != 8 is a diagnostic build (front-end role alone, WAKEWORD_FUSED_EXP=1)"
+#endif
+constexpr int kFeWaves = WK_FE_WAVES;
 constexpr int kFusedBlock = 1024;    // 8 front-end + 8 CNN waves
 // LDS carve after the front-end's (wk_fe_dev.h): fixed tail, then the CNN
 // images [clip][t][ci] -- fp32, or bf16 for bf16 convolutions -- overlaying
@@ -188,9 +195,9 @@ __device__ __forceinline__ void spin_until(unsigned* ctrl, int idx, unsigned v) 
 // Barrier among the 8 waves of one role (LDS counter; s_barrier would also
 // stop the other role's waves).  LDS operations of a wave complete in order,
 // so a wave's data writes are visible before its arrival is.
-template <int PRIO>
+template <int PRIO, int N = 8>
 __device__ __forceinline__ void role_sync(unsigned* ctrl, int idx, unsigned& gen, int lane) {
-  gen += 8;
+  gen += N;
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(ctrl + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -228,11 +235,15 @@ __device__ __forceinline__ void signal_add(unsigned* ctrl, int idx, int lane) {
 
 // ---------------------------------------------------------------------------
 // Front-end role (waves 0-7): mode B (torchaudio + CMVN), one clip at a time.
+// FEW = 12 (diagnostic builds only, WK_FE_WAVES): 12 front-end waves, 3 per
+// SIMD -- waves 0-3 run rounds 0 and 1 of frame slot w, waves 4-7 round 0 of
+// slot w, waves 8-11 round 1 of slot w - 4; the mel stays 8-way, on waves 4-11.
 // ---------------------------------------------------------------------------
-template <typename T>
+template <typename T, int FEW = 8>
 __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio, int64_t n_mine,
                                         int64_t clip_stride, float* __restrict__ feats_out, int wave, int lane,
                                         int diag) {
+  static_assert(FEW == 8 || FEW == 12, "8 or 12 front-end waves");
   float* P = smem + kPOff;
   float* L = smem + kLOff;
   float* L1 = smem + kL1Off;
@@ -242,7 +253,11 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   const TwsLds tws = {smem + kTwsOff};
   const f2 w0 = fe_split_tw(j, 0);
   const int slot_base = 16 * (g & 1) + 32 * (g >> 1);
-  const int fw = wave;   // frame slot of this wave (moving the edge frames to other waves measured neutral)
+  // frame slot of this wave (moving the edge frames to other waves measured neutral), its rounds r0..r1
+  const int fw = FEW == 8 || wave < 8 ? wave : wave - 4;
+  const int r0 = FEW == 8 || wave < 8 ? 0 : 1, r1 = FEW == 8 || wave < 4 ? 1 : r0;
+  const bool mel_wave = FEW == 8 || wave >= 4;
+  const int melw = FEW == 8 ? wave : wave - 4;
   const int64_t G = gridDim.x;
   unsigned gen = 0, p_wait = 0;
 
@@ -277,13 +292,13 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
 
   Raw<T> pf;
   {
-    const PfCtx c0 = pf_ctx(cptr, n_mine > 0, 0);
+    const PfCtx c0 = pf_ctx(cptr, n_mine > 0, r0);
     load_raw<true>(c0.rs, c0.base, j, kWinSamples, true, c0.general, pf);
   }
   WK_STAMP_INIT
   for (int64_t i = 0; i < n_mine; ++i) {
 #pragma unroll 1
-    for (int r = 0; r < 2; ++r) {
+    for (int r = r0; r <= r1; ++r) {
       const int fl = fw + 8 * r + slot_base;   // == frame index t (one chunk per clip)
       const bool general = (r == 0 && fw == 0) || (r == 1 && fw == 6);
       f2 a[16];
@@ -295,8 +310,8 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       // the prefetch parts issued from inside fe_rest load for all lanes.
       fe_stage0<true>(pf, 256 * fl - 160, kWinSamples, j, general, tb, a);
       WK_STAMP(0);
-      // next round: (i, 1) after round 0, (i + 1, 0) after round 1
-      const PfCtx nx = r == 0 ? pf_ctx(cptr, true, 1) : pf_ctx(cptr + step, i + 1 < n_mine, 0);
+      // next round: (i, 1) after round 0, (i + 1, 0) after round 1 (one-round waves: (i + 1, r0))
+      const PfCtx nx = r < r1 ? pf_ctx(cptr, true, r + 1) : pf_ctx(cptr + step, i + 1 < n_mine, r0);
       // k = -1: the round is about to write its first power-row element.  In
       // round 0 that needs every wave done reading clip i-1's rows (its mel);
       // waiting there rather than before the round lets stage 0, the loads and
@@ -304,7 +319,7 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       auto pf_part = [&](int k) {
         if (k >= 0) {
           load_raw_part<true>(nx.rs, nx.base, j, kWinSamples, true, nx.general, pf, k);
-        } else if (r == 0) {
+        } else if (r == r0) {
           spin_until<kPrioFe>(ctrl, kCtrlFeBar, p_wait);
           WK_STAMP(9);
         }
@@ -313,24 +328,24 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
       float* row = fl < kNFramesB ? P + fl * kPRow : smem + kDummyRowOff;
       fe_rest<true>(a, j, row, row + (fl & 1), tb, w0, tws, 0, pf_part WK_SP_ARG);
     }
-    role_sync<kPrioFe>(ctrl, kCtrlFeBar, gen, lane);                    // all power rows of clip i written
+    role_sync<kPrioFe, FEW>(ctrl, kCtrlFeBar, gen, lane);               // all power rows of clip i written
     WK_STAMP(7);
-    if (i >= 2 && !(diag & 1)) spin_until_all8<kPrioFe>(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
+    if (mel_wave && i >= 2 && !(diag & 1)) spin_until_all8<kPrioFe>(ctrl, kCtrlLFree, (unsigned)(i - 1));   // clip i-2's DCT done
     WK_STAMP(10);
-    {
+    if (mel_wave) {
       // The row base stays opaque (one VGPR with kPOff in it), so the mel's
       // power reads take bin offsets as read2 immediates; folded into the
       // immediates, kPOff pushed them past read2's 255-dword reach and every
       // pair of reads cost a v_add_u32 for its address.
       int prow = kPOff + min(lane, kNFramesB - 1) * kPRow;
       asm volatile("" : "+v"(prow));
-      mel_dispatch<true>(wave, smem + prow, (i & 1 ? L1 : L) + lane);
+      mel_dispatch<true>(melw, smem + prow, (i & 1 ? L1 : L) + lane);
+      WK_STAMP(8);
+      signal_add(ctrl, kCtrlLReady, lane);
     }
-    WK_STAMP(8);
-    signal_add(ctrl, kCtrlLReady, lane);
     // Split barrier: arrive now, wait before this wave next writes a power
-    // row (round 0 of clip i+1), after its stage 0 and prefetch.
-    gen += 8;
+    // row (its first round of clip i+1), after its stage 0 and prefetch.
+    gen += FEW;
     signal_add(ctrl, kCtrlFeBar, lane);
     p_wait = gen;
     cptr += step;
@@ -807,9 +822,9 @@ __global__ __launch_bounds__(kFusedBlock, 4) void wk_fused_kernel(const T* __res
   // The front-end role is the critical path: static issue priority over the
   // CNN role measured +0.5-0.9 % (priority 1-3); the reverse (CNN over
   // front-end) measured -13 %.
-  if (wave < 8) __builtin_amdgcn_s_setprio(kPrioFe);
-  if (wave < 8) {
-    if (!(diag & 2)) fe_role<T>(smem, audio, n_mine, clip_stride, feats_out, wave, lane, diag);
+  if (wave < kFeWaves) __builtin_amdgcn_s_setprio(kPrioFe);
+  if (wave < kFeWaves) {
+    if (!(diag & 2)) fe_role<T, kFeWaves>(smem, audio, n_mine, clip_stride, feats_out, wave, lane, diag);
   } else {
     if (!(diag & 1)) {
       LogmelSrc<CM, FEATS> src = {smem, reinterpret_cast<unsigned*>(smem + kCtrlOff), feats_out, (int64_t)blockIdx.x,
