@@ -293,6 +293,29 @@ def load_traffic(precision="fp32"):
         return None, None
 
 
+def load_utilisation(precision="fp32"):
+    """Datapath shares of the fused kernel from the committed rocprofv3 --pmc
+    summary that hbm_traffic*.json names (VALU and MFMA
+    utilisation beside the HBM figure).  Kernel cycles = GRBM_GUI_ACTIVE / 8
+    XCDs; valu_active = SQ_ACTIVE_INST_VALU x 4 / (1,024 SIMDs x cycles),
+    mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1,024 x cycles).  None if absent."""
+    tf = "hbm_traffic.json" if precision == "fp32" else f"hbm_traffic_{precision}.json"
+    cm = {"fp32": 0, "bf16": 1, "bf16x3": 2}[precision]
+    try:
+        with open(os.path.join(REPO, "profiles", tf)) as fh:
+            src = json.load(fh)["source"].split()[0]
+        with open(os.path.join(REPO, src)) as fh:
+            d = json.load(fh)
+        k = next(v for n, v in d.items() if n.startswith(f"wk_fused_kernel<float, {cm}, false>"))
+        cyc = k["GRBM_GUI_ACTIVE"] / 8.0
+        return {"valu_active": round(k["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * cyc), 3),
+                "mfma_busy": round(k["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * cyc), 3),
+                "eff_clock_ghz": round(k["eff_clock_ghz"], 3) if k.get("eff_clock_ghz") else None,
+                "source": src}
+    except (OSError, ValueError, KeyError, StopIteration):
+        return None
+
+
 def init_rank(args, env, torch, dist):
     """This rank's (world, rank, local device, shared) from torchrun's
     environment, with the process group formed: nccl (RCCL) with the rank's
@@ -445,6 +468,9 @@ def main():
                 out["roofline"][k] = None
         if traffic_src:
             out["roofline"]["traffic_source"] = traffic_src
+        util = load_utilisation(args.precision)
+        if util:
+            out["roofline"]["utilisation"] = util
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         if world == 1 and not shared and not args.no_extras:

@@ -144,3 +144,15 @@ def test_host_threads_reports_affinity():
     assert affinity == len(os.sched_getaffinity(0))
     assert 1 <= threads <= affinity
     assert quota is None or threads <= quota
+
+
+def test_committed_profiles_feed_the_bench_line():
+    """The roofline's traffic and utilisation come from committed rocprofv3
+    PMC summaries (profiles/): both present for fp32 and bf16, shares in (0, 1]."""
+    for prec in ("fp32", "bf16"):
+        bpw, src = bench.load_traffic(prec)
+        assert bpw and 64_004 * 0.99 < bpw < 64_004 * 1.1, (prec, bpw)
+        u = bench.load_utilisation(prec)
+        assert u is not None and u["source"].startswith("profiles/")
+        assert 0.0 < u["valu_active"] <= 2.0 and 0.0 < u["mfma_busy"] <= 1.0
+    assert bench.FLOP_PER_WINDOW == 2_262_440   # SURVEY 8(d)
