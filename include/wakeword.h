@@ -54,7 +54,7 @@ typedef enum { WK_DTYPE_F32 = 0, WK_DTYPE_I16 = 1, WK_DTYPE_I8 = 2 } wk_dtype;  
  * front-end.  BF16X3 = fp32-grade convolutions on bf16 MFMA: activations and
  * weights split into bf16 hi + lo parts, products hi*hi + hi*lo + lo*hi
  * accumulated in fp32 (relative product error ~2^-16); same logit tolerance
- * as FP32.  BF16 and BF16X3 run in the fused kernel (wk_forward) only. */
+ * as FP32.  Every precision runs in wk_forward and in wk_cnn. */
 typedef enum { WK_PREC_FP32 = 0, WK_PREC_BF16 = 1, WK_PREC_INT8 = 2, WK_PREC_BF16X3 = 3 } wk_precision;
 
 typedef struct {
