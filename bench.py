@@ -476,13 +476,17 @@ def main():
         if world == 1 and not shared and not args.no_extras:
             # SURVEY 8(d) configs 4, 5, 3, measured after the headline's timed
             # region and its CPU leg (the headline above is unchanged by them)
+            # (a Python-level failure in one of them is recorded in its key; the
+            # headline line is printed regardless)
             del clips
-            torch.cuda.empty_cache()
-            out["config4"] = extra_config4(torch, wakeword, _lib, local, args.seed)
-            torch.cuda.empty_cache()
-            out["config5"] = extra_config5(local)
-            torch.cuda.empty_cache()
-            out["config3"] = extra_config3(wakeword, local)
+            for key, fn in (("config4", lambda: extra_config4(torch, wakeword, _lib, local, args.seed)),
+                            ("config5", lambda: extra_config5(local)),
+                            ("config3", lambda: extra_config3(wakeword, local))):
+                torch.cuda.empty_cache()
+                try:
+                    out[key] = fn()
+                except Exception as e:   # noqa: BLE001 -- reported, not hidden
+                    out[key] = {"error": f"{type(e).__name__}: {e}"}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -311,3 +311,23 @@ def test_config5_decision_parity(precision, out_scale, mix, monkeypatch):
     # confident frames decide exactly as the oracle does (the fp16 margin wherever an fp16 stage is in the path)
     bound = CTC_FLIP_MARGIN["fp16" if precision == "fp16" or "out16" in mix else "fp32"]
     assert margins.numel() == 0 or float(margins.max()) <= bound, float(margins.max())
+
+
+@pytest.mark.gpu
+def test_bench_line_carries_every_config(gpu):
+    """The driver's bench line (bench.py, N = 1) holds the headline and the
+    config 4 / 5 / 3 keys, each measured (no error entry)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0
+    for key in ("config4", "config5", "config3"):
+        assert key in line and "error" not in line[key], (key, line.get(key))
+    assert line["config4"]["batch_per_gpu"] == 131_072 and line["config4"]["value"] > 0
+    assert line["config5"]["value"] > 0 and line["config5"]["output_kernel"]["frac"] > 0
+    assert line["config3"]["p50_latency_ms"] > 0
