@@ -29,6 +29,9 @@ constexpr int kFeBlock = 512;        // 8 waves per front-end workgroup
 // arithmetic as scalar fp32 pairs (v_fma/v_add/v_mul_f32; swaps and signs are
 // register choices and VOP3 neg modifiers), no packed ops -- beside the bf16
 // MFMAs those issue faster (wk_fused.hip header).
+// It also issues the real-FFT split stage by stage across each group of
+// chains (wk_fe_dev.h fe_rest).
+#define WK_FE_STAGED 1
 struct __attribute__((aligned(8))) f2 {
   float x, y;
 };
@@ -44,6 +47,7 @@ __device__ __forceinline__ f2 bx(f2 a) { return {a.x, a.x}; }
 __device__ __forceinline__ f2 by(f2 a) { return {a.y, a.y}; }
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return {__builtin_fmaf(a.x, b.x, c.x), __builtin_fmaf(a.y, b.y, c.y)}; }
 #else
+#define WK_FE_STAGED 0
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 swp(f2 a) { return __builtin_shufflevector(a, a, 1, 0); }
@@ -65,6 +69,19 @@ __device__ __forceinline__ f2 cmul2(f2 a, f2 w) {
   f2 r;
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
   return r;
+}
+// cmul2 in two phases, t = cmul2_a(a, w) then cmul2_b(a, w, t), for a group
+// of independent products issued phase by phase (WK_FE_STAGED): the same
+// operations as cmul2, so the same bits.
+__device__ __forceinline__ f2 cmul2_a(f2 a, f2 w) { return a * bx(w); }
+__device__ __forceinline__ f2 cmul2_b(f2 a, f2 w, f2 t) {
+#if defined(WK_FE_SCALAR) && defined(WK_FUSED_TU)
+  return {__builtin_fmaf(-a.y, w.y, t.x), __builtin_fmaf(a.x, w.y, t.y)};
+#else
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
+#endif
 }
 // a * w for a compile-time constant w.
 __device__ __forceinline__ f2 cmulc(f2 a, f2 w) { return fma2(swp(a), f2{-w.y, w.y}, a * f2{w.x, w.x}); }

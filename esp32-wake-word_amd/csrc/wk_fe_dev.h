@@ -305,10 +305,39 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
   // time, stage by stage, so independent ops fill each other's latency
   // (left to itself the scheduler emitted them back to back, one chain at a
   // time, with s_nop between dependent v_pk ops).
+  // WK_FE_STAGED (the bf16-family unit's scalar front-end, wk_common.h) also
+  // issues the group's DPP moves and each chain stage across the group: the
+  // same operations per value, bit-identical, bf16 +0.8 % (profiles/
+  // r06m_staged_ab.txt); the packed fp32 unit measured -0.1 % with it, so
+  // it keeps the per-chain order.
   constexpr int G = 3;
 #pragma unroll
   for (int k0 = 0; k0 < 8; k0 += G) {
     f2 S[G], D[G], pw[G];
+#if WK_FE_STAGED
+    // the partners' row_mirror moves of the group first, then their row_shr
+    // moves (a DPP read of a VGPR written by the previous VALU op waits 2 states)
+    float mx[G], my[G];
+#pragma unroll
+    for (int t = 0; t < G; ++t)
+      if (k0 + t <= 7) {
+        const f2 sv = c[dft16_out(15 - k0 - t)];
+        mx[t] = dpp<0x140>(sv.x);
+        my[t] = dpp<0x140>(sv.y);
+      }
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const int k2 = k0 + t;
+      if (k2 > 7) continue;
+      const f2 zk = c[dft16_out(k2)];
+      const f2 own = c[dft16_out((16 - k2) & 15)];
+      f2 zq;
+      zq.x = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.x), __float_as_int(mx[t]), 0x111, 0xF, 0xF, false));
+      zq.y = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), __float_as_int(my[t]), 0x111, 0xF, 0xF, false));
+      S[t] = fma2(zq, f2{1.0f, -1.0f}, zk);
+      D[t] = fma2(zq, f2{-1.0f, 1.0f}, zk);
+    }
+#else
 #pragma unroll
     for (int t = 0; t < G; ++t) {
       const int k2 = k0 + t;
@@ -327,6 +356,36 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
       S[t] = fma2(zq, f2{1.0f, -1.0f}, zk);
       D[t] = fma2(zq, f2{-1.0f, 1.0f}, zk);
     }
+#endif
+#if WK_FE_STAGED
+    // the G chains issued stage by stage (the same operations per value)
+    f2 wt[G], tt[G], bb[G], uvx[G], uvy[G], sq[G];
+#pragma unroll
+    for (int t = 0; t < G; ++t)
+      if (k0 + t <= 7) {
+        wt[t] = k0 + t == 0 ? w0 : tws(k0 + t, j);
+        tt[t] = cmul2_a(D[t], wt[t]);
+      }
+#pragma unroll
+    for (int t = 0; t < G; ++t)
+      if (k0 + t <= 7) bb[t] = cmul2_b(D[t], wt[t], tt[t]);
+#pragma unroll
+    for (int t = 0; t < G; ++t)
+      if (k0 + t <= 7) {
+        uvx[t] = fma2(by(bb[t]), f2{1.0f, -1.0f}, bx(S[t]));
+        uvy[t] = fma2(bx(bb[t]), f2{-1.0f, 1.0f}, by(S[t]));
+      }
+#pragma unroll
+    for (int t = 0; t < G; ++t)
+      if (k0 + t <= 7) sq[t] = uvy[t] * uvy[t];
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const int k2 = k0 + t;
+      if (k2 > 7) continue;
+      pw[t] = fma2(uvx[t], uvx[t], sq[t]);
+      if constexpr (!MODE_B) pw[t] = fma2(pw[t], k2 == 0 ? sc0 : sc, f2{1e-12f, 1e-12f});
+    }
+#else
 #pragma unroll
     for (int t = 0; t < G; ++t) {
       const int k2 = k0 + t;
@@ -337,6 +396,7 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
       pw[t] = fma2(uvx, uvx, uvy * uvy);
       if constexpr (!MODE_B) pw[t] = fma2(pw[t], k2 == 0 ? sc0 : sc, f2{1e-12f, 1e-12f});
     }
+#endif
     // the group's low bins first, then its high bins: same-base stores 16
     // dwords apart, back to back, which the compiler pairs into ds_write2_b32
 #pragma unroll
