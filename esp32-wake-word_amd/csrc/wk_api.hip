@@ -549,17 +549,17 @@ void analyze_mfcc_range(float* mfcc, int size, const char* label) {
 // stream samples [k*hop, k*hop + 16000); a push completes every window whose
 // end it reaches; windows whose start was already overwritten are dropped.
 //
-// Latency path (a push that completes a few windows, the real-time case): the
-// ring and the logits live in pinned, mapped host memory, and the fused
-// kernel reads the window straight from the host ring and writes the logit
-// straight into host memory -- one kernel launch and one wait per push, no
-// copy commands.  A push that completes more than kZeroCopyMax windows (a
-// backlog) copies the run's samples to device memory first, so the kernel
-// reads HBM rather than re-reading overlapping windows across PCIe.
+// The mirrored ring is in device memory.  A push writes its samples once into
+// a pinned, mapped host staging ring of `cap` (same positions); a push that
+// completes windows first launches wk_ring_ingest_kernel, which reads the
+// samples pushed since the last launch (only the newest `cap`: older ones are
+// overwritten, and no window left to score starts there) across PCIe into both
+// copies of the device ring, then the fused kernel reads its windows from HBM
+// and writes the logits straight into pinned host memory -- two launches and
+// one wait per push, no copy commands.  (Reading each window across PCIe
+// instead, zero-copy from a mirrored host ring, cost ~9 us per window: one
+// workgroup's loads over PCIe latency; a hop of new samples is one round trip.)
 // ---------------------------------------------------------------------------
-namespace {
-constexpr int64_t kZeroCopyMax = 4;
-}
 
 struct wk_stream {
   wk_handle* h;
@@ -567,9 +567,10 @@ struct wk_stream {
   int32_t hop, cap;
   int64_t total;        // samples pushed since create / reset
   int64_t next_win;     // index of the next window to score
-  float* h_ring;        // pinned, mapped [2*cap] (written by the host, read by the kernel)
+  int64_t ingested;     // stream samples [0, ingested) are in d_ring (as far as it holds them)
+  float* h_ring;        // pinned, mapped [cap] staging ring (written by the host, read by the ingest kernel)
   float* a_ring;        // device alias of h_ring
-  float* d_stage;       // device [2*cap]: backlog runs are copied here first
+  float* d_ring;        // device [2*cap], mirrored: sample p at p % cap and p % cap + cap
   float* h_logits;      // pinned, mapped [max_win] (written by the kernel)
   float* a_logits;      // device alias of h_logits
   unsigned* h_err;      // pinned, mapped: this stream object's own error word (its pushes' launches only)
@@ -579,7 +580,7 @@ struct wk_stream {
 
 static void stream_free(wk_stream* s) {
   (void)hipHostFree(s->h_ring);
-  (void)hipFree(s->d_stage);
+  (void)hipFree(s->d_ring);
   (void)hipHostFree(s->h_logits);
   (void)hipHostFree(s->h_err);
   free(s);
@@ -601,9 +602,9 @@ wk_status wk_stream_create(wk_handle* h, int32_t hop, int32_t capacity, void* st
     s->max_win = (capacity - WK_WIN_SAMPLES) / hop + 1;
     const unsigned mapped = hipHostMallocMapped | hipHostMallocCoherent;
     hipError_t e;
-    if ((e = hipHostMalloc(&s->h_ring, sizeof(float) * 2 * (size_t)capacity, mapped)) != hipSuccess ||
+    if ((e = hipHostMalloc(&s->h_ring, sizeof(float) * (size_t)capacity, mapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&s->a_ring, s->h_ring, 0)) != hipSuccess ||
-        (e = hipMalloc(&s->d_stage, sizeof(float) * 2 * (size_t)capacity)) != hipSuccess ||
+        (e = hipMalloc(&s->d_ring, sizeof(float) * 2 * (size_t)capacity)) != hipSuccess ||
         (e = hipHostMalloc(&s->h_logits, sizeof(float) * (size_t)s->max_win, mapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&s->a_logits, s->h_logits, 0)) != hipSuccess ||
         (e = hipHostMalloc(&s->h_err, sizeof(unsigned), mapped)) != hipSuccess ||
@@ -611,7 +612,7 @@ wk_status wk_stream_create(wk_handle* h, int32_t hop, int32_t capacity, void* st
       stream_free(s);
       return e == hipErrorOutOfMemory ? WK_ERR_NO_MEMORY : hip_fail(e, "wk_stream_create");
     }
-    memset(s->h_ring, 0, sizeof(float) * 2 * (size_t)capacity);
+    memset(s->h_ring, 0, sizeof(float) * (size_t)capacity);
     *s->h_err = 0;
     *out = s;
     return WK_OK;
@@ -631,6 +632,7 @@ wk_status wk_stream_reset(wk_stream* s) {
   if (!s) return invalid("wk_stream_reset: null stream");
   s->total = 0;
   s->next_win = 0;
+  s->ingested = 0;
   return WK_OK;
 }
 
@@ -640,17 +642,16 @@ wk_status wk_stream_push(wk_stream* s, const float* samples, int64_t n, float* o
     return invalid("wk_stream_push: bad arguments");
   *n_out = 0;
   // Every push that launches work waits for it before returning, so no kernel
-  // is reading the host ring while it is rewritten here.
+  // is reading the host staging ring while it is rewritten here.
   const int64_t cap = s->cap;
   // 1. ring write (overwrite-oldest): only the newest `cap` samples of a long push survive.
   const int64_t skip = n > cap ? n - cap : 0;
   const int64_t m = n - skip;
   const int64_t p0 = s->total + skip;
-  for (int64_t done = 0; done < m;) {   // at most two segments (wrap), each written twice (mirror)
+  for (int64_t done = 0; done < m;) {   // at most two segments (wrap)
     const int64_t pos = (p0 + done) % cap;
     const int64_t len = m - done < cap - pos ? m - done : cap - pos;
     memcpy(s->h_ring + pos, samples + skip + done, sizeof(float) * (size_t)len);
-    memcpy(s->h_ring + pos + cap, samples + skip + done, sizeof(float) * (size_t)len);
     done += len;
   }
   s->total += n;
@@ -675,25 +676,20 @@ wk_status wk_stream_push(wk_stream* s, const float* samples, int64_t n, float* o
       }
     } drain{s->st};
     hipError_t e;
+    // the samples pushed since the last launch that the staging ring still holds
+    const int64_t from = s->ingested > s->total - cap ? s->ingested : s->total - cap;
+    drain.armed = true;
+    if ((e = wk::launch_ring_ingest(s->a_ring, s->d_ring, cap, from % cap, s->total - from, s->st)) != hipSuccess)
+      return hip_fail(e, "wk_stream_push: ingest");
+    s->ingested = s->total;
     int64_t w = first;
     while (w <= last) {
-      drain.armed = true;
       const int64_t off = (w * s->hop) % cap;
       int64_t run = (2 * cap - WK_WIN_SAMPLES - off) / s->hop + 1;   // windows that fit before the mirror end
       if (run > last - w + 1) run = last - w + 1;
-      const float* src = s->a_ring + off;
-      if (run > kZeroCopyMax) {   // backlog: one copy of the run's span to HBM, then score from there
-        const int64_t span = (run - 1) * s->hop + WK_WIN_SAMPLES;
-        if ((e = hipMemcpyAsync(s->d_stage, s->h_ring + off, sizeof(float) * (size_t)span, hipMemcpyHostToDevice,
-                                s->st)) != hipSuccess)
-          return hip_fail(e, "wk_stream_push: H2D");
-        src = s->d_stage;
-      }
-      wk_status st = forward_impl(s->h, src, WK_DTYPE_F32, run, WK_WIN_SAMPLES, s->hop, s->a_logits + (w - first),
-                                  nullptr, s->st, s->d_err);
+      wk_status st = forward_impl(s->h, s->d_ring + off, WK_DTYPE_F32, run, WK_WIN_SAMPLES, s->hop,
+                                  s->a_logits + (w - first), nullptr, s->st, s->d_err);
       if (st != WK_OK) return st;
-      if (run > kZeroCopyMax && (e = hipStreamSynchronize(s->st)) != hipSuccess)   // d_stage is reused
-        return hip_fail(e, "wk_stream_push: sync");
       w += run;
     }
     if ((e = hipStreamSynchronize(s->st)) != hipSuccess) return hip_fail(e, "wk_stream_push: sync");

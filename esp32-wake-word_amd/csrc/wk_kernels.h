@@ -68,6 +68,8 @@ hipError_t launch_normalize(const float* in, float* out, int64_t batch, int n_co
 // The firmware's per-window CMVN over an MFCC frame stream (wk_device_cmvn).
 hipError_t launch_record_front(const int16_t* tdm, int64_t n_out, int16_t* out16, float* outf, hipStream_t stream);
 hipError_t launch_quantize_frames(const float* x, int64_t n, int8_t* q, hipStream_t stream);
+// wk_stream_push: ring samples [pos, pos + m) mod cap, host staging ring -> mirrored device ring.
+hipError_t launch_ring_ingest(const float* src, float* dst, int64_t cap, int64_t pos, int64_t m, hipStream_t stream);
 hipError_t launch_device_cmvn(const void* frames, bool int8_in, int64_t n_windows, int8_t* out_i8, float* out_f,
                               hipStream_t stream);
 

@@ -171,9 +171,31 @@ __global__ __launch_bounds__(256) void wk_quantize_frames_kernel(const float* __
     q[i] = (int8_t)device_q(x[i]);
 }
 
+// Streaming ring ingest (wk_stream_push): ring samples [pos, pos + m) (mod
+// cap, m <= cap) from the pinned host staging ring, read across PCIe, into
+// both copies of the mirrored device ring.
+__global__ __launch_bounds__(256) void wk_ring_ingest_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                             int64_t cap, int64_t pos, int64_t m) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = pos + i < cap ? pos + i : pos + i - cap;
+    const float v = src[p];
+    dst[p] = v;
+    dst[p + cap] = v;
+  }
+}
+
 }  // namespace
 
 namespace wk {
+
+hipError_t launch_ring_ingest(const float* src, float* dst, int64_t cap, int64_t pos, int64_t m, hipStream_t stream) {
+  if (m <= 0) return hipSuccess;
+  if (pos < 0 || pos >= cap || m > cap) return hipErrorInvalidValue;
+  int64_t blocks = (m + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wk_ring_ingest_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, src, dst, cap, pos, m);
+  return hipGetLastError();
+}
 
 hipError_t launch_record_front(const int16_t* tdm, int64_t n_out, int16_t* out16, float* outf, hipStream_t stream) {
   if (n_out <= 0) return hipSuccess;

@@ -140,10 +140,11 @@ wk_status wk_normalize(const float* d_in, float* d_out, int64_t batch, int32_t n
  * newest max_out are scored) with the fused path on the handle's device, and
  * returns their logits and end positions (samples since create/reset) in host
  * memory.  It blocks until the logits are on the host.  Not thread-safe per
- * stream object.  The ring and the logits live in pinned, mapped host memory:
- * a push that completes up to 4 windows is one kernel launch that reads the
- * window from the host ring and writes the logits to host memory directly (no
- * copy commands); larger backlogs are copied to device memory first. */
+ * stream object.  The ring lives in device memory behind a pinned host
+ * staging ring; a push that completes windows is two launches and one wait:
+ * a small kernel reads the samples pushed since the last such push across
+ * PCIe into the device ring, then the fused kernel scores the windows from
+ * HBM and writes the logits to pinned host memory (no copy commands). */
 typedef struct wk_stream wk_stream;
 wk_status wk_stream_create(wk_handle* h, int32_t hop, int32_t capacity, void* stream, wk_stream** out);
 wk_status wk_stream_destroy(wk_stream* s);
