@@ -43,6 +43,22 @@ for i in range(300):
     st.synchronize()
     ts.append((time.perf_counter() - t0) * 1e6)
 print(f"wk_forward + sync wall: p50 {np.percentile(ts[20:], 50):.1f} us")
+ts = []
+for i in range(300):
+    t0 = time.perf_counter()
+    fwd()
+    while not st.query():
+        pass
+    ts.append((time.perf_counter() - t0) * 1e6)
+print(f"wk_forward + spin on hipStreamQuery wall: p50 {np.percentile(ts[20:], 50):.1f} us")
+for name, wait in (("sync", st.synchronize), ("spin", lambda: [None for _ in iter(st.query, True)])):
+    ts = []
+    for i in range(300):
+        t0 = time.perf_counter()
+        lg.zero_()
+        wait()
+        ts.append((time.perf_counter() - t0) * 1e6)
+    print(f"trivial kernel (fill) + {name} wall: p50 {np.percentile(ts[20:], 50):.1f} us")
 det = wakeword.StreamingDetector(m, hop=480)
 audio = wakeword.synth_clips(1234, 0, 20).reshape(-1).cpu().numpy()
 det.push(audio[:16000])
