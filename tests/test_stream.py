@@ -116,3 +116,35 @@ def test_stream_overwrite_oldest_and_reset(model):
         got += [w.logit for w in det.push(audio[p:p + hop])]
     np.testing.assert_array_equal(np.asarray(got, np.float32), ref)
     det.close()
+
+
+@pytest.mark.gpu
+def test_stream_deferred_ingest(model):
+    """Pushes that score nothing (max_out = 0) launch nothing, so their samples
+    reach the device ring at the next push that scores windows: across more
+    than a ring's worth of such pushes, that push's windows equal the batch
+    path's bit for bit."""
+    import ctypes as C
+    import wakeword
+    from wakeword import _lib
+    hop, cap = 480, WIN + 6 * 480
+    audio = _stream_audio(4)
+    ref = _batch_logits(model, audio, hop)
+    det = wakeword.StreamingDetector(model, hop=hop, capacity=cap)
+    L = _lib.lib()
+    logits, ends = np.zeros(64, np.float32), np.zeros(64, np.int64)
+    n = C.c_int32(0)
+    split = audio.size - 3 * 480   # silent pushes up to here (> cap samples), then one scoring push
+    for p in range(0, split, 1000):
+        x = np.ascontiguousarray(audio[p:min(p + 1000, split)])
+        _lib.check(L.wk_stream_push(det._s, x.ctypes.data_as(C.POINTER(C.c_float)), x.size,
+                                    logits.ctypes.data_as(C.POINTER(C.c_float)),
+                                    ends.ctypes.data_as(C.POINTER(C.c_int64)), 0, C.byref(n)), "wk_stream_push")
+        assert n.value == 0
+    assert split > cap
+    out = det.push(audio[split:])   # scores the windows this push completes
+    first, last = (split - WIN) // hop + 1, (audio.size - WIN) // hop
+    assert last - first + 1 == 3
+    assert [w.end for w in out] == [WIN + k * hop for k in range(first, last + 1)]
+    np.testing.assert_array_equal(np.asarray([w.logit for w in out], np.float32), ref[first:last + 1])
+    det.close()
