@@ -260,6 +260,12 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
   wave_lds_sync();
 #pragma unroll
   for (int s = 0; s < 8; ++s) c[s] = x2[j + 17 * s];
+  // The packed unit issues prefetch parts 2 and 3 one step earlier than the
+  // scalar unit (after these reads, and before the second DFT16 rather than
+  // after it): the loads get ~1 k more cycles to land before the next round
+  // needs them, fp32 +0.8 % (8 of 8 alternating passes, profiles/
+  // r06u_prefetch_ab.txt); the scalar unit measured -0.5 to 0 % with it.
+  if constexpr (!WK_FE_STAGED) pf(2);
 #pragma unroll
   for (int s = 8; s < 16; ++s) b[s - 8] = tw(s);
   wave_lds_sync();
@@ -271,9 +277,14 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
   wave_lds_sync();
   WK_FE_HIT(4);
 
-  pf(2);
-  dft16(c);  // +-Z[j + 16*k2] at c[dft16_out(k2)]
-  pf(3);
+  if constexpr (WK_FE_STAGED) {
+    pf(2);
+    dft16(c);  // +-Z[j + 16*k2] at c[dft16_out(k2)]
+    pf(3);
+  } else {
+    pf(3);
+    dft16(c);
+  }
   WK_FE_HIT(5);
 
   // Real-FFT split, k = j + 16*k2 (k2 = 0..7), with the partner Z[256 - k]:
