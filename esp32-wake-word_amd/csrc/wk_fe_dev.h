@@ -90,10 +90,15 @@ __device__ __forceinline__ void load_raw(__amdgpu_buffer_rsrc_t rs, int base, in
   }
 }
 
-// Part k (0..3) of load_raw: rows n1 in [3k, 3k+3) (and xb with part 0), so
-// a round's prefetch can be spread over the round instead of issued as one
-// burst (eight waves issuing 11 loads each at once filled the TA FIFOs and
+// Part k (0..3) of load_raw: rows n1 with pf_part(n1) == k (and xb with part
+// 0), so a round's prefetch can be spread over the round instead of issued as
+// one burst (eight waves issuing 11 loads each at once filled the TA FIFOs and
 // stalled issue).  The edge-frame (GENERAL) form is issued whole with part 0.
+// The packed unit front-loads the parts (rows 0-3, 4-6, 7-8, 9) and issues
+// them earlier in the round (fe_rest); the scalar unit issues rows 3k..3k+2.
+__device__ __forceinline__ constexpr int pf_part(int n1) {
+  return WK_FE_STAGED ? n1 / 3 : (n1 < 4 ? 0 : n1 < 7 ? 1 : n1 < 9 ? 2 : 3);
+}
 template <bool MODE_B, typename T>
 __device__ __forceinline__ void load_raw_part(__amdgpu_buffer_rsrc_t rs, int base, int j, int n, bool act,
                                               bool general, Raw<T>& r, int part) {
@@ -105,7 +110,7 @@ __device__ __forceinline__ void load_raw_part(__amdgpu_buffer_rsrc_t rs, int bas
   const int v0 = base + 2 * j;
 #pragma unroll
   for (int n1 = 0; n1 < 10; ++n1)
-    if (n1 / 3 == part) raw_ld2<T>(rs, v0 + 32 * n1, r.x0[n1], r.x1[n1]);
+    if (pf_part(n1) == part) raw_ld2<T>(rs, v0 + 32 * n1, r.x0[n1], r.x1[n1]);
   if (part == 0) r.xb = raw_ld<T>(rs, base - 1);
 }
 
@@ -249,22 +254,24 @@ __device__ __forceinline__ void fe_rest(f2 (&a)[16], int j, float* __restrict__ 
   const int wb = 17 * (j & 7) + (j & 8);
   auto tw = [&](int s) { return cmul2(a[dft16_out(s)], *reinterpret_cast<const f2*>(tb.tw + (s * 16 + j) * 2)); };
   f2 b[8];
+  if constexpr (!WK_FE_STAGED) pf(1);
 #pragma unroll
   for (int s = 0; s < 8; ++s) b[s] = tw(s);
   pf(-1);   // the first write into this frame's LDS row follows (fused kernel: wait until the row is free)
 #pragma unroll
   for (int s = 0; s < 8; ++s) x2[wb + s] = b[s];
   WK_FE_HIT(3);
-  pf(1);
+  if constexpr (WK_FE_STAGED) pf(1);
   f2 c[16];
   wave_lds_sync();
 #pragma unroll
   for (int s = 0; s < 8; ++s) c[s] = x2[j + 17 * s];
-  // The packed unit issues prefetch parts 2 and 3 one step earlier than the
-  // scalar unit (after these reads, and before the second DFT16 rather than
-  // after it): the loads get ~1 k more cycles to land before the next round
-  // needs them, fp32 +0.8 % (8 of 8 alternating passes, profiles/
-  // r06u_prefetch_ab.txt); the scalar unit measured -0.5 to 0 % with it.
+  // The packed unit issues prefetch parts 1-3 one step earlier than the
+  // scalar unit (part 1 before the twiddles, part 2 after these reads, part 3
+  // before the second DFT16 rather than after it): the loads get ~1 k more
+  // cycles to land before the next round needs them; with the front-loaded
+  // parts, fp32 +1.5 % (profiles/r06u..r06x); the scalar unit
+  // measured -0.5 to 0 % with the earlier parts 2-3.
   if constexpr (!WK_FE_STAGED) pf(2);
 #pragma unroll
   for (int s = 8; s < 16; ++s) b[s - 8] = tw(s);
