@@ -685,6 +685,10 @@ __device__ __forceinline__ void cnn_role(float* base, const float* __restrict__ 
       const int bo = li * I2_CIP;
 #pragma unroll 1
       for (int p = 0; p < 2; ++p) {
+        // between conv3's two passes too: the longest phase, during which the
+        // front-end otherwise waited on the log-mel buffer (fp32 +1.1 %, bf16
+        // +0.6 %, profiles/r06ac_eager_ab.txt; inside conv2 as well spilled, -0.6 %)
+        if (p > 0) try_eager(b);
         const int ca = 2 * p, cb = 2 * p + 1;
         if (ca >= nv) break;
         f32x4 acc_a = {0, 0, 0, 0}, acc_b = {0, 0, 0, 0};
