@@ -285,9 +285,16 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
     int base;       // first sample of the lane group's frame (before reflection)
     bool general;   // edge frame: per-lane reflected indices, issued whole with part 0
   };
+  // Frame slot of round r.  The bf16-family unit (scalar front-end) swaps
+  // round 1's slots between waves w and w ^ 4, so its second edge frame (62)
+  // runs on wave 2 rather than wave 6: waves 4-7 issue after 0-3 on each SIMD
+  // and reach the power-row barrier last, wave 6 with the edge frame latest.
+  // bf16 +0.8 %; the packed fp32 unit measured -0.8 % with it
+  // (profiles/r06ae_round1_swap_ab.txt).  Bit-identical either way.
+  auto fwr = [&](int r) { return FEW == 8 && WK_FE_STAGED && r == 1 ? fw ^ 4 : fw; };
   auto pf_ctx = [&](const T* p, bool ok, int r) -> PfCtx {
-    const int fl = fw + 8 * r + slot_base;
-    return {make_rsrc(p, ok ? kClipBytes : 0u), 256 * fl - 160, (r == 0 && fw == 0) || (r == 1 && fw == 6)};
+    const int fl = fwr(r) + 8 * r + slot_base;
+    return {make_rsrc(p, ok ? kClipBytes : 0u), 256 * fl - 160, (r == 0 && fwr(r) == 0) || (r == 1 && fwr(r) == 6)};
   };
 
   Raw<T> pf;
@@ -299,8 +306,8 @@ __device__ __forceinline__ void fe_role(float* smem, const T* __restrict__ audio
   for (int64_t i = 0; i < n_mine; ++i) {
 #pragma unroll 1
     for (int r = r0; r <= r1; ++r) {
-      const int fl = fw + 8 * r + slot_base;   // == frame index t (one chunk per clip)
-      const bool general = (r == 0 && fw == 0) || (r == 1 && fw == 6);
+      const int fl = fwr(r) + 8 * r + slot_base;   // == frame index t (one chunk per clip)
+      const bool general = (r == 0 && fwr(r) == 0) || (r == 1 && fwr(r) == 6);
       f2 a[16];
 #ifdef WK_DIAG
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: time the wait for the prefetched audio apart
