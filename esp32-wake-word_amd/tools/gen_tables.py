@@ -29,6 +29,9 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(os.path.dirname(HERE), "csrc", "wk_tables.h")
 N_WAVES = 8
+# Relative mel speed per wave (fused kernel: the front-end waves 0-3 issue
+# ahead of 4-7 on each SIMD).
+MEL_WAVE_WEIGHTS = [1.0] * N_WAVES
 N_MELS = 40
 N_MFCC = 13
 
@@ -118,8 +121,10 @@ def dct_mode_a() -> np.ndarray:
     return cos
 
 
-def partition(fb: np.ndarray, n_parts: int):
-    """Contiguous split of the filters minimising max(distinct bins + fmas)."""
+def partition(fb: np.ndarray, n_parts: int, weights=None):
+    """Contiguous split of the filters minimising max(cost / weight) over the
+    parts, cost = distinct bins + fmas (+ 12 per filter); part p goes to wave p."""
+    weights = weights or [1.0] * n_parts
     nz = [np.nonzero(fb[:, m])[0] for m in range(fb.shape[1])]
 
     def cost(a, b):
@@ -138,7 +143,7 @@ def partition(fb: np.ndarray, n_parts: int):
     for p in range(1, n_parts + 1):
         for b in range(1, M + 1):
             for a in range(p - 1, b):
-                v = max(dp[p - 1][a], cost(a, b))
+                v = max(dp[p - 1][a], cost(a, b) / weights[p - 1])
                 if v < dp[p][b]:
                     dp[p][b], cut[p][b] = v, a
     bounds = []
@@ -152,8 +157,9 @@ def partition(fb: np.ndarray, n_parts: int):
 
 def emit_mel(fb: np.ndarray, name: str, mode: str, scale: float):
     """One straight-line function per wave: P row -> log-mel row."""
-    bounds, worst = partition(fb, N_WAVES)
-    lines = [f"// {name}: filters per wave {bounds}, worst-wave cost {worst}"]
+    env = os.environ.get("WK_MEL_WEIGHTS")
+    bounds, worst = partition(fb, N_WAVES, [float(v) for v in env.split(",")] if env else MEL_WAVE_WEIGHTS)
+    lines = [f"// {name}: filters per wave {bounds}, worst-wave cost {worst:.4g}"]
     for w, (a, b) in enumerate(bounds):
         lines.append(f"__device__ __forceinline__ void {name}_w{w}(const float* __restrict__ p, float* __restrict__ l) {{")
         for m in range(a, b):
