@@ -29,8 +29,10 @@ constexpr int kFeBlock = 512;        // 8 waves per front-end workgroup
 // arithmetic as scalar fp32 pairs (v_fma/v_add/v_mul_f32; swaps and signs are
 // register choices and VOP3 neg modifiers), no packed ops -- beside the bf16
 // MFMAs those issue faster (wk_fused.hip header).
-// It also issues the real-FFT split stage by stage across each group of
-// chains (wk_fe_dev.h fe_rest).
+// WK_FE_STAGED marks this unit wherever the two units' front-end schedules
+// differ, each measured in its own unit: the real-FFT split
+// issued stage by stage across each group of chains and the prefetch
+// placement (wk_fe_dev.h fe_rest), the round-1 frame slots (wk_fused.hip).
 #define WK_FE_STAGED 1
 struct __attribute__((aligned(8))) f2 {
   float x, y;
